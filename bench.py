@@ -1,0 +1,286 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched ICP scan-pairs/s (1081-point scans) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Workload (BASELINE.json configs[2], "Batched ICP: 10k synthetic scan-pairs x
+1081 pts"): every rank holds its own synthetic scan stream of P+1 scans
+(P = 10,000 by default; SURVEY.md §8(d) generator, seed 2025 + rank) already
+resident in HBM and runs ``icp()`` on the P consecutive pairs (i, i-1) with
+scripts/main.py's parameters (init = pose_to_mat(odom_i - odom_{i-1}),
+epsilon 0.05, max_iters 100).  One step = one ``slam_icp_batch_f64`` launch
+over the rank's P pairs and, for N > 1, the RCCL all-gather of the resulting
+SE(2) edges (the exchange step of the north star).  Per-GPU work is fixed as N
+grows ("scaling": "weak"); ``--strong`` shards one P-pair stream instead.
+
+Printed: ONE JSON line (rank 0) with the driver's contract fields plus
+``roofline`` (dominant kernel vs the fp64 VALU roofline, HBM rate beside it),
+``cpu_baseline`` (NumPy port of the reference, timed on this host) and
+secondary pose-graph numbers (``pgo``).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+
+FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (spec), MI355X_MICROARCH.md
+HBM_PEAK_GBPS = 8000.0
+ISSUE_BOUND_EVALS = 256 * 2.4e9 * 64 / 8   # ~8 VALU issue slots per candidate
+FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add (exact NumPy order)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--pairs", type=int, default=10000, help="scan pairs per rank (weak) or total (--strong)")
+    p.add_argument("--beams", type=int, default=1081)
+    p.add_argument("--strong", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pgo", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=48, help="pairs in the CPU baseline sample")
+    p.add_argument("--cpu-workers", type=int, default=16)
+    p.add_argument("--instance", type=int, default=-1, help="force a kernel instance (diagnostics)")
+    return p.parse_args()
+
+
+def init_dist(args):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def make_workload(args, world, rank):
+    from slamhip import se2, synthetic
+    if args.strong:
+        total = args.pairs
+        per = (total + world - 1) // world
+        lo = min(rank * per, total)
+        hi = min(lo + per, total)
+        seq = synthetic.make_sequence(total + 1, seed=2025, n_beams=args.beams)
+        scans = seq.scans[lo:hi + 1]
+        odo = seq.odometry[lo:hi + 1]
+    else:
+        seq = synthetic.make_sequence(args.pairs + 1, seed=2025 + rank, n_beams=args.beams)
+        scans, odo = seq.scans, seq.odometry
+    n = len(scans) - 1
+    inits = np.stack([se2.pose_to_mat(odo[i] - odo[i - 1]) for i in range(1, n + 1)]) if n else np.zeros((0, 3, 3))
+    return scans, inits
+
+
+def cpu_baseline(scans, inits, sample, workers):
+    """NumPy port of the reference (per-query loop of src/icp.py:16-17, same
+    arithmetic as the reference), fanned out with joblib loky like
+    scripts/main.py:240 — on `workers` host cores."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from joblib import Parallel, delayed
+    import icp_oracle
+
+    def one(pc1, pc2, init):
+        h, e = icp_oracle.icp(pc1, pc2, init, 0.05, 100, corr_fn=icp_oracle.correspondences_loop)
+        return len(h) - 1
+
+    idx = np.linspace(0, len(inits) - 1, sample).astype(int)
+    jobs = [(np.c_[scans[i + 1], np.ones(len(scans[i + 1]))], np.c_[scans[i], np.ones(len(scans[i]))],
+             inits[i].copy()) for i in idx]
+    env = {"OMP_NUM_THREADS": "1", "OPENBLAS_NUM_THREADS": "1", "MKL_NUM_THREADS": "1"}
+    os.environ.update(env)
+    par = Parallel(n_jobs=workers, backend="loky")
+    par(delayed(one)(*jobs[0]) for _ in range(min(workers, 4)))   # spin the pool up
+    t0 = time.perf_counter()
+    its = par(delayed(one)(*j) for j in jobs)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample / dt, 3), "unit": "scan-pairs/s", "cores": workers, "kind": "port",
+            "sample": f"{sample} pairs of this workload (1081-pt scans, mean {np.mean(its):.1f} ICP iterations), "
+                      f"oracle/icp_oracle.py with the reference's per-query loop, joblib loky x{workers} "
+                      f"(scripts/main.py:240 pattern), {dt:.1f} s wall"}
+
+
+def pgo_bench():
+    """Secondary: SGD relaxation step on the C4-size graph (5,000 nodes)."""
+    import torch
+    from slamhip import pgo, synthetic
+    import src.pose_graph as pgm
+    poses, loops = synthetic.lap_pose_graph(side_len=3.0, poses_per_side=125, num_loops=10, seed=0,
+                                            num_constraints=15000)
+    pg = pgm.PoseGraph(poses.copy())
+    for a, b in loops:
+        pg.add_constraint(a, b, np.eye(3))
+    ea, eb, tf = pg.edge_arrays()
+    s = pgo.SgdSolver(poses, ea, eb, tf)
+    s.step(1.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    k = 3
+    for i in range(k):
+        s.step(1.0 / (i + 2))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    out = {"sgd_step_ms": round(dt * 1e3, 3), "sgd_graph": f"{len(poses)} nodes / {len(ea)} edges",
+           "sgd_ref_cpu_s_per_step": 138.9}
+    try:
+        from slamhip import gn
+        out.update(gn.bench_c4())
+    except (ImportError, AttributeError):
+        pass
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    world, rank, local = init_dist(args)
+    if world > 1:
+        import torch.distributed as dist
+    from slamhip import _abi
+    from slamhip import icp as k
+
+    t_gen = time.perf_counter()
+    scans, inits = make_workload(args, world, rank)
+    B = len(inits)
+    log(f"[rank {rank}] generated {B} pairs in {time.perf_counter() - t_gen:.1f}s")
+    lib = _abi.lib()
+    if args.instance >= 0:
+        lib.slam_icp_force_instance(args.instance)
+    ss = k.ScanSet(scans)
+    batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)
+    gathered = None
+    if world > 1:
+        gathered = torch.empty((world, max(B, 1), 11), dtype=torch.float64, device=ss.device)
+
+    stream = torch.cuda.current_stream()
+
+    def step():
+        batch.launch()
+        if world > 1:
+            # SE(2) edges + error + iteration count of every pair -> every rank
+            local_res = torch.cat([batch.out_tf[:max(B, 1)], batch.out_err[:max(B, 1)].unsqueeze(1),
+                                   batch.out_iters[:max(B, 1)].to(torch.float64).unsqueeze(1)], dim=1)
+            dist.all_gather_into_tensor(gathered, local_res)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        batch.launch()
+        ev[i][1].record(stream)
+        if world > 1:
+            local_res = torch.cat([batch.out_tf[:max(B, 1)], batch.out_err[:max(B, 1)].unsqueeze(1),
+                                   batch.out_iters[:max(B, 1)].to(torch.float64).unsqueeze(1)], dim=1)
+            dist.all_gather_into_tensor(gathered, local_res)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    res = batch.result()
+    n1 = ss.lens[1:B + 1]
+    n2 = ss.lens[0:B]
+    evals = float(np.sum(res.iters * n1 * n2))
+    t = torch.tensor([dt, evals, float(B), float(res.iters.sum())], dtype=torch.float64, device=ss.device)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t[0] = tmax[0]
+    dt_max, evals_all, pairs_all, iters_all = [float(x) for x in t.cpu()]
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = dt_max / args.steps * 1e3
+    value = pairs_all * args.steps / dt_max
+    # dominant kernel: slam_icp_batch_f64 on rank 0 (its own pairs)
+    flops = FLOP_PER_EVAL * evals / (kern_ms * 1e-3) / 1e12
+    alg_bytes = 16.0 * float(ss.lens.sum()) + B * (4 + 4 + 72 + 72 + 8 + 4) + 8 * (len(ss.lens) + 1)
+    hbm_gbps = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("icp_batch_bytes_per_launch")
+        except Exception:
+            traffic = None
+    sel = lib.slam_icp_selected_instance(int(n1.max()))
+    import ctypes
+    bb, qq = ctypes.c_int32(), ctypes.c_int32()
+    lib.slam_icp_instance_shape(sel, ctypes.byref(bb), ctypes.byref(qq))
+    out = {
+        "metric": "ICP scan-pairs/sec (1081-pt scans)",
+        "value": round(value, 2),
+        "unit": "scan-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8(d) ray-cast room, 1081 beams/270 deg, 0.01 m noise; EECS_3 unavailable offline)",
+        "config": {"workload": "C3 batched ICP: consecutive scan pairs of a synthetic stream, "
+                               "scripts/main.py params (eps 0.05, max_iters 100)",
+                   "pairs_per_rank": B, "pairs_total": int(pairs_all), "points_per_scan": int(n1.max()),
+                   "mean_icp_iterations": round(iters_all / pairs_all, 3),
+                   "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}"},
+        "roofline": {
+            "bound": "valu",
+            "kernel": "slam_icp_batch_f64 (icp_kernel)",
+            "achieved": round(flops, 3),
+            "peak": FP64_VALU_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(flops / FP64_VALU_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "kernel_ms": round(kern_ms, 4),
+            "candidate_evals_per_launch": evals,
+            "issue_bound_frac": round(evals / (kern_ms * 1e-3) / ISSUE_BOUND_EVALS, 4),
+            "hbm": {"achieved": round(hbm_gbps, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(hbm_gbps / HBM_PEAK_GBPS, 6), "algorithmic_bytes_per_launch": alg_bytes},
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(scans, inits, args.cpu_sample, args.cpu_workers)
+        except Exception as e:   # keep the GPU line even if the host pool fails
+            out["cpu_baseline"] = {"error": repr(e)}
+    if world == 1 and not args.no_pgo:
+        try:
+            out["pgo"] = pgo_bench()
+        except Exception as e:
+            out["pgo"] = {"error": repr(e)}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

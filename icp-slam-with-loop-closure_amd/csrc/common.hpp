@@ -1,0 +1,104 @@
+// common.hpp — shared helpers of the slamhip C-ABI (error state, launch checks).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "slamhip.h"
+
+namespace slamhip {
+
+// Thread-local message of the last failing call (slam_last_error()).
+inline char* last_error_buf() {
+    static thread_local char buf[512] = {0};
+    return buf;
+}
+
+inline int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(last_error_buf(), 512, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+inline int ok() {
+    last_error_buf()[0] = 0;
+    return SLAM_OK;
+}
+
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SLAM_EHIP, "%s: %s", what, hipGetErrorString(e));
+    return ok();
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// 3x3 SE(2) matrix with the last row implicit [0, 0, 1].
+struct SE2 {
+    double m00, m01, m02, m10, m11, m12;
+};
+
+__device__ __forceinline__ SE2 load_se2(const double* p) {
+    SE2 t;
+    t.m00 = p[0]; t.m01 = p[1]; t.m02 = p[2];
+    t.m10 = p[3]; t.m11 = p[4]; t.m12 = p[5];
+    return t;
+}
+
+__device__ __forceinline__ void store_se2(double* p, const SE2& t) {
+    p[0] = t.m00; p[1] = t.m01; p[2] = t.m02;
+    p[3] = t.m10; p[4] = t.m11; p[5] = t.m12;
+    p[6] = 0.0;   p[7] = 0.0;   p[8] = 1.0;
+}
+
+// A @ B for SE(2) matrices with NumPy/OpenBLAS dgemm rounding: every entry is
+// the k = 0, 1, 2 FMA chain fma(a2, b2, fma(a1, b1, a0 * b0)) (verified bit
+// for bit against numpy 2.2 / OpenBLAS 0.3.29 in the build container).  With
+// B's last row [0, 0, 1] the k = 2 term is +0 (columns 0, 1) or a2 (column 2).
+__device__ __forceinline__ SE2 se2_mul(const SE2& a, const SE2& b) {
+    SE2 c;
+    c.m00 = fma(a.m02, 0.0, fma(a.m01, b.m10, a.m00 * b.m00));
+    c.m01 = fma(a.m02, 0.0, fma(a.m01, b.m11, a.m00 * b.m01));
+    c.m02 = fma(a.m02, 1.0, fma(a.m01, b.m12, a.m00 * b.m02));
+    c.m10 = fma(a.m12, 0.0, fma(a.m11, b.m10, a.m10 * b.m00));
+    c.m11 = fma(a.m12, 0.0, fma(a.m11, b.m11, a.m10 * b.m01));
+    c.m12 = fma(a.m12, 1.0, fma(a.m11, b.m12, a.m10 * b.m02));
+    return c;
+}
+
+// All-lane sum of a wave64 by xor butterfly: every lane ends with the same
+// bits (each stage adds the same two operands, only commuted).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Deterministic block all-reduce of NV doubles; `red` is LDS scratch of
+// WAVES * NV doubles.  Every thread returns identical bits (fixed wave order).
+template <int NV, int WAVES>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[wave * NV + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = red[k];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) s += red[w * NV + k];
+        v[k] = s;
+    }
+}
+
+}  // namespace slamhip

@@ -1,0 +1,437 @@
+// icp_kernels.hip — batched 2-D point-to-point ICP for gfx950 (MI355X).
+//
+// Rebuilds the hot path of the reference's src/icp.py (cohnt/ICP-SLAM-with-
+// Loop-Closure) as one fused kernel: ONE scan pair per workgroup, every ICP
+// iteration on chip, transform history streamed out.
+//
+//   reference                               here
+//   src/icp.py:62   np.dot(T, pc1.T).T      transform_queries(): FMA chain in
+//                                           OpenBLAS dgemm order (bit-equal)
+//   src/icp.py:4-19 get_correspondences     nn_scan(): exact fp64 distance
+//                                           (dx*dx + dy*dy, no contraction),
+//                                           strict-< ascending scan = np.argmin
+//                                           first-minimum rule; pc2 resident in
+//                                           LDS, read as broadcast ds_read_b128
+//   src/icp.py:22-46 get_transform          two deterministic block reductions
+//                                           (centroids, then the centred 2x2
+//                                           cross-covariance) + closed-form 2x2
+//                                           Kabsch (argmax_R tr(R S))
+//   src/icp.py:49-52 get_error              sum of the per-query minima
+//   src/icp.py:72-97 icp() loop             stopping rules evaluated on chip,
+//                                           identically by every thread
+//
+// Compile with -ffp-contract=off: the distance must round exactly like NumPy.
+// MFMA is deliberately not used: the work is a min-reduction, not a
+// contraction, and is bound by fp64 VALU issue.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace slamhip {
+
+constexpr int kCandCap = 4096;        // pc2 points resident in LDS (64 KiB)
+constexpr int kRedDoubles = 2 * 8 * 9;  // two reduction slabs, <= 8 waves x 9
+
+struct IcpArgs {
+    const double2* pts;
+    const int64_t* scan_off;
+    const int32_t* src_scan;
+    const int32_t* dst_scan;
+    const double* init;
+    double epsilon;
+    double stopping_thresh;
+    int32_t max_iters;
+    int32_t rotation_only;
+    int32_t cand_cap;       // LDS candidate capacity for this launch (points)
+    int32_t hist_stride;
+    double* out_hist;
+    double* out_tf;
+    double* out_err;
+    int32_t* out_iters;
+    // single-step mode
+    int64_t* out_corr;
+    const int64_t* corr_off;
+};
+
+// Exhaustive first-minimum nearest neighbour of QPT queries per lane against
+// `cnt` candidates in LDS (all lanes read the same candidate: broadcast).
+template <int QPT>
+__device__ __forceinline__ void nn_scan(const double2* __restrict__ cand, int cnt, int base,
+                                        const double (&qx)[QPT], const double (&qy)[QPT],
+                                        double (&best)[QPT], int (&bi)[QPT]) {
+#pragma unroll 2
+    for (int j = 0; j < cnt; ++j) {
+        const double2 p = cand[j];
+        const int jj = base + j;
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const double dx = p.x - qx[k];
+            const double dy = p.y - qy[k];
+            const double d = dx * dx + dy * dy;   // NumPy: sum((pc - point)**2, axis=1)
+            const bool lt = d < best[k];
+            best[k] = lt ? d : best[k];
+            bi[k] = lt ? jj : bi[k];
+        }
+    }
+}
+
+template <int BLOCK, int QPT, bool STEP>
+__global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
+    constexpr int WAVES = BLOCK / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* red0 = reinterpret_cast<double*>(smem);
+    double* red1 = red0 + WAVES * 8;
+    double2* cand = reinterpret_cast<double2*>(smem + kRedDoubles * sizeof(double));
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int s1 = a.src_scan[b];
+    const int s2 = a.dst_scan[b];
+    const int64_t o1 = a.scan_off[s1];
+    const int64_t o2 = a.scan_off[s2];
+    const int n1 = static_cast<int>(a.scan_off[s1 + 1] - o1);
+    const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
+    const double2* __restrict__ p1 = a.pts + o1;
+    const double2* __restrict__ p2 = a.pts + o2;
+    const int cap = a.cand_cap;
+    const bool resident = n2 <= cap;
+
+    if (resident) {
+        for (int j = tid; j < n2; j += BLOCK) cand[j] = p2[j];
+    }
+
+    SE2 T = load_se2(a.init + 9 * static_cast<int64_t>(b));
+    if (a.rotation_only) {   // src/icp.py:60-61 zeroes previous_transform[:2, 2]
+        T.m02 = 0.0;
+        T.m12 = 0.0;
+    }
+    double* hist = (!STEP && a.hist_stride > 0)
+                       ? a.out_hist + static_cast<int64_t>(b) * a.hist_stride * 9
+                       : nullptr;
+    if (hist && tid == 0) store_se2(hist, T);
+    __syncthreads();
+
+    double last_err = 0.0;
+    for (int it = 0;; ++it) {
+        // ---- src/icp.py:62  pc1_transformed = T @ pc1 -------------------------
+        double qx[QPT], qy[QPT], best[QPT];
+        int bi[QPT];
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const int i = k * BLOCK + tid;
+            double x = 0.0, y = 0.0;
+            if (i < n1) {
+                const double2 p = p1[i];
+                x = p.x;
+                y = p.y;
+            }
+            qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));
+            qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+            best[k] = INFINITY;
+            bi[k] = 0;
+        }
+
+        // ---- src/icp.py:63  correspondences (exhaustive NN) -------------------
+        if (resident) {
+            nn_scan<QPT>(cand, n2, 0, qx, qy, best, bi);
+        } else {
+            for (int t0 = 0; t0 < n2; t0 += cap) {
+                const int cnt = min(cap, n2 - t0);
+                __syncthreads();
+                for (int j = tid; j < cnt; j += BLOCK) cand[j] = p2[t0 + j];
+                __syncthreads();
+                nn_scan<QPT>(cand, cnt, t0, qx, qy, best, bi);
+            }
+        }
+
+        // ---- src/icp.py:64,68  centroids + error ------------------------------
+        double bx[QPT], by[QPT];
+        double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const int i = k * BLOCK + tid;
+            bx[k] = 0.0;
+            by[k] = 0.0;
+            if (i < n1) {
+                const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
+                bx[k] = m.x;
+                by[k] = m.y;
+                v[0] += qx[k];
+                v[1] += qy[k];
+                v[2] += m.x;
+                v[3] += m.y;
+                v[4] += best[k];   // == (pc1_t - pc2[corr])**2 summed over the row
+            }
+        }
+        block_sum<5, WAVES>(v, red0);
+        const double n = static_cast<double>(n1);
+        const double mux = v[0] / n, muy = v[1] / n;     // pc1_avg
+        const double mvx = v[2] / n, mvy = v[3] / n;     // pc2_avg
+        const double err = v[4];
+
+        // ---- S = X @ Y.T over centred rows ------------------------------------
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const int i = k * BLOCK + tid;
+            if (i < n1) {
+                const double xa = qx[k] - mux, ya = qy[k] - muy;
+                const double xb = bx[k] - mvx, yb = by[k] - mvy;
+                s[0] = fma(xa, xb, s[0]);
+                s[1] = fma(xa, yb, s[1]);
+                s[2] = fma(ya, xb, s[2]);
+                s[3] = fma(ya, yb, s[3]);
+            }
+        }
+        block_sum<4, WAVES>(s, red1);
+
+        // ---- closed-form 2x2 Kabsch: R maximising tr(R S) ---------------------
+        // Equals V diag(1, det(V U^T)) U^T of the reference's SVD route.
+        const double cs = s[0] + s[3];
+        const double sn = s[1] - s[2];
+        const double r = sqrt(cs * cs + sn * sn);
+        const double c = r > 0.0 ? cs / r : 1.0;
+        const double si = r > 0.0 ? sn / r : 0.0;
+        // t = pc2_avg - R @ pc1_avg (dgemv order)
+        double tx = mvx - fma(-si, muy, c * mux);
+        double ty = mvy - fma(c, muy, si * mux);
+        if (a.rotation_only) {   // src/icp.py:65-66
+            tx = 0.0;
+            ty = 0.0;
+        }
+        SE2 D;
+        D.m00 = c;  D.m01 = -si; D.m02 = tx;
+        D.m10 = si; D.m11 = c;   D.m12 = ty;
+        const SE2 Tn = se2_mul(D, T);   // src/icp.py:67
+
+        if constexpr (STEP) {
+            if (tid == 0) {
+                store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                a.out_err[b] = err;
+            }
+            int64_t* corr = a.out_corr + a.corr_off[b];
+#pragma unroll
+            for (int k = 0; k < QPT; ++k) {
+                const int i = k * BLOCK + tid;
+                if (i < n1) corr[i] = bi[k];
+            }
+            return;
+        } else {
+            if (hist && tid == 0) store_se2(hist + 9 * (it + 1), Tn);
+            // src/icp.py:86-95 (identical in every thread -> uniform exit)
+            const bool stop = (err < a.epsilon) || (it > a.max_iters) ||
+                              (it > 0 && fabs(last_err - err) < a.stopping_thresh);
+            last_err = err;
+            T = Tn;
+            if (stop) {
+                if (tid == 0) {
+                    store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                    a.out_err[b] = err;
+                    a.out_iters[b] = it + 1;
+                }
+                return;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Instance table.  A (BLOCK, QPT) instance holds BLOCK*QPT queries in
+// registers; the host picks the smallest capacity >= max_n1 so idle lanes stay
+// few (1081-point scans: 64x17 = 1088 -> 99.4 % of lanes busy).
+// ---------------------------------------------------------------------------
+using KernelFn = void (*)(IcpArgs);
+
+struct Instance {
+    int block;
+    int qpt;
+    KernelFn batch;
+    KernelFn step;
+};
+
+#define SLAM_INST(B, Q) {B, Q, icp_kernel<B, Q, false>, icp_kernel<B, Q, true>}
+static const Instance kInstances[] = {
+    SLAM_INST(64, 1),   SLAM_INST(64, 2),   SLAM_INST(64, 4),   SLAM_INST(64, 8),
+    SLAM_INST(64, 12),  SLAM_INST(64, 17),  SLAM_INST(128, 9),  SLAM_INST(128, 12),
+    SLAM_INST(128, 16), SLAM_INST(256, 5),  SLAM_INST(256, 8),  SLAM_INST(256, 12),
+    SLAM_INST(256, 16), SLAM_INST(512, 16),
+};
+#undef SLAM_INST
+constexpr int kNumInstances = sizeof(kInstances) / sizeof(kInstances[0]);
+constexpr int kMaxQuery = 512 * 16;
+
+static const Instance* pick_instance(int max_n1, int forced) {
+    if (forced >= 0 && forced < kNumInstances) return &kInstances[forced];
+    const Instance* bestp = nullptr;
+    for (int i = 0; i < kNumInstances; ++i) {
+        const Instance& c = kInstances[i];
+        const int capq = c.block * c.qpt;
+        if (capq < max_n1) continue;
+        if (!bestp) { bestp = &c; continue; }
+        const int bcap = bestp->block * bestp->qpt;
+        if (capq < bcap || (capq == bcap && c.block < bestp->block)) bestp = &c;
+    }
+    return bestp;
+}
+
+static int g_forced_instance = -1;
+
+// get_transform + get_error on already-matched rows (src/icp.py:22-52), one
+// workgroup; the same reductions and closed form as the fused kernel.
+constexpr int kKabschBlock = 256;
+__global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __restrict__ pa,
+                                                              const double2* __restrict__ pb,
+                                                              int64_t n, double* out_T,
+                                                              double* out_err) {
+    constexpr int WAVES = kKabschBlock / 64;
+    __shared__ double red[2 * WAVES * 5];
+    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int64_t i = threadIdx.x; i < n; i += kKabschBlock) {
+        const double2 p = pa[i], q = pb[i];
+        const double dx = p.x - q.x, dy = p.y - q.y;
+        v[0] += p.x;
+        v[1] += p.y;
+        v[2] += q.x;
+        v[3] += q.y;
+        v[4] += dx * dx + dy * dy;
+    }
+    block_sum<5, WAVES>(v, red);
+    const double nn = static_cast<double>(n);
+    const double mux = v[0] / nn, muy = v[1] / nn, mvx = v[2] / nn, mvy = v[3] / nn;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t i = threadIdx.x; i < n; i += kKabschBlock) {
+        const double2 p = pa[i], q = pb[i];
+        const double xa = p.x - mux, ya = p.y - muy, xb = q.x - mvx, yb = q.y - mvy;
+        s[0] = fma(xa, xb, s[0]);
+        s[1] = fma(xa, yb, s[1]);
+        s[2] = fma(ya, xb, s[2]);
+        s[3] = fma(ya, yb, s[3]);
+    }
+    block_sum<4, WAVES>(s, red + WAVES * 5);
+    if (threadIdx.x == 0) {
+        const double cs = s[0] + s[3], sn = s[1] - s[2];
+        const double r = sqrt(cs * cs + sn * sn);
+        const double c = r > 0.0 ? cs / r : 1.0;
+        const double si = r > 0.0 ? sn / r : 0.0;
+        SE2 D;
+        D.m00 = c;  D.m01 = -si; D.m02 = mvx - fma(-si, muy, c * mux);
+        D.m10 = si; D.m11 = c;   D.m12 = mvy - fma(c, muy, si * mux);
+        store_se2(out_T, D);
+        *out_err = v[4];
+    }
+}
+
+static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
+                  void* stream) {
+    const Instance* inst = pick_instance(max_n1, g_forced_instance);
+    if (!inst) return fail(SLAM_ETOOBIG, "query scan of %d points exceeds capacity %d", max_n1, kMaxQuery);
+    IcpArgs a = args;
+    a.cand_cap = max_n2 < kCandCap ? (max_n2 > 0 ? max_n2 : 1) : kCandCap;
+    const size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
+    KernelFn fn = step ? inst->step : inst->batch;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        static_cast<int>(lds));
+    hipLaunchKernelGGL(fn, dim3(B), dim3(inst->block), lds,
+                       as_stream(stream), a);
+    return check_launch(step ? "icp_step kernel" : "icp_batch kernel");
+}
+
+}  // namespace slamhip
+
+using namespace slamhip;
+
+extern "C" {
+
+int slam_abi_version(void) { return 100; }
+
+const char* slam_last_error(void) { return last_error_buf(); }
+
+int slam_icp_max_query_points(void) { return kMaxQuery; }
+
+// Diagnostics: number of compiled (BLOCK, QPT) instances, their shapes, and a
+// way to force one (bench/profile sweeps).  Not part of the stable ABI.
+int slam_icp_num_instances(void) { return kNumInstances; }
+int slam_icp_instance_shape(int i, int* block, int* qpt) {
+    if (i < 0 || i >= kNumInstances) return fail(SLAM_EINVAL, "instance %d out of range", i);
+    *block = kInstances[i].block;
+    *qpt = kInstances[i].qpt;
+    return ok();
+}
+int slam_icp_force_instance(int i) {
+    g_forced_instance = (i >= 0 && i < kNumInstances) ? i : -1;
+    return ok();
+}
+int slam_icp_selected_instance(int max_n1) {
+    const Instance* p = pick_instance(max_n1, g_forced_instance);
+    return p ? static_cast<int>(p - kInstances) : -1;
+}
+
+int slam_icp_batch_f64(const double* pts, const int64_t* scan_off, const int32_t* src_scan,
+                       const int32_t* dst_scan, const double* init, int32_t B, double epsilon,
+                       int32_t max_iters, double stopping_thresh, int32_t rotation_only,
+                       int32_t max_n1, int32_t max_n2, int32_t hist_stride, double* out_hist,
+                       double* out_tf, double* out_err, int32_t* out_iters, void* stream) {
+    if (B < 0) return fail(SLAM_EINVAL, "B = %d < 0", B);
+    if (B == 0) return ok();
+    if (!pts || !scan_off || !src_scan || !dst_scan || !init || !out_tf || !out_err || !out_iters)
+        return fail(SLAM_EINVAL, "null array argument");
+    if (max_n1 < 1 || max_n2 < 1) return fail(SLAM_EINVAL, "empty scan (max_n1=%d, max_n2=%d)", max_n1, max_n2);
+    if (max_iters > 1000000) return fail(SLAM_EINVAL, "max_iters %d > 1e6", max_iters);
+    if (hist_stride < 0 || (hist_stride > 0 && (hist_stride < max_iters + 3 || !out_hist)))
+        return fail(SLAM_EINVAL, "hist_stride %d must be 0 or >= max_iters + 3 (%d)", hist_stride, max_iters + 3);
+    IcpArgs a{};
+    a.pts = reinterpret_cast<const double2*>(pts);
+    a.scan_off = scan_off;
+    a.src_scan = src_scan;
+    a.dst_scan = dst_scan;
+    a.init = init;
+    a.epsilon = epsilon;
+    a.stopping_thresh = stopping_thresh;
+    a.max_iters = max_iters < -1 ? -1 : max_iters;
+    a.rotation_only = rotation_only;
+    a.hist_stride = hist_stride;
+    a.out_hist = out_hist;
+    a.out_tf = out_tf;
+    a.out_err = out_err;
+    a.out_iters = out_iters;
+    return launch(false, a, B, max_n1, max_n2, stream);
+}
+
+int slam_icp_step_f64(const double* pts, const int64_t* scan_off, const int32_t* src_scan,
+                      const int32_t* dst_scan, const double* T_in, int32_t B, int32_t rotation_only,
+                      int32_t max_n1, int32_t max_n2, double* T_out, int64_t* out_corr,
+                      const int64_t* corr_off, double* out_err, void* stream) {
+    if (B < 0) return fail(SLAM_EINVAL, "B = %d < 0", B);
+    if (B == 0) return ok();
+    if (!pts || !scan_off || !src_scan || !dst_scan || !T_in || !T_out || !out_corr || !corr_off || !out_err)
+        return fail(SLAM_EINVAL, "null array argument");
+    if (max_n1 < 1 || max_n2 < 1) return fail(SLAM_EINVAL, "empty scan (max_n1=%d, max_n2=%d)", max_n1, max_n2);
+    IcpArgs a{};
+    a.pts = reinterpret_cast<const double2*>(pts);
+    a.scan_off = scan_off;
+    a.src_scan = src_scan;
+    a.dst_scan = dst_scan;
+    a.init = T_in;
+    a.rotation_only = rotation_only;
+    a.out_tf = T_out;
+    a.out_err = out_err;
+    a.out_corr = out_corr;
+    a.corr_off = corr_off;
+    return launch(true, a, B, max_n1, max_n2, stream);
+}
+
+int slam_kabsch2d_f64(const double* a, const double* b, int64_t n, double* out_T, double* out_err,
+                      void* stream) {
+    if (n < 1) return fail(SLAM_EINVAL, "kabsch2d: n = %lld < 1", static_cast<long long>(n));
+    if (!a || !b || !out_T || !out_err) return fail(SLAM_EINVAL, "null array argument");
+    hipLaunchKernelGGL(kabsch_kernel, dim3(1), dim3(kKabschBlock), 0, as_stream(stream),
+                       reinterpret_cast<const double2*>(a), reinterpret_cast<const double2*>(b), n,
+                       out_T, out_err);
+    return check_launch("kabsch2d kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,402 @@
+// pgo_kernels.hip — SE(2) pose-graph relaxation kernels for gfx950 (MI355X).
+//
+// Rebuilds src/pose_graph_optimization.py (cohnt/ICP-SLAM-with-Loop-Closure):
+//
+//   pose_graph_optimization_step_sgd  (:7-49)
+//     pass 1 (:13-24)  sgd_weights_kernel: M[i] = sum over loop edges e with
+//                      a_e < i <= b_e of diag(W_e), accumulated in edge order
+//                      (one thread per node, so every M[i] is the reference's
+//                      sequential sum), W_e = inv(R sigma R^T); gamma = the
+//                      first minimum-norm diag(W_e) (sgd_gamma_kernel).
+//     pass 2 (:27-49)  sgd_relax_kernel: ONE persistent workgroup walks the
+//                      loop edges in networkx order (each edge reads poses the
+//                      previous edges moved — a true sequential dependency) and
+//                      spreads the residual over (a, b] with a block-wide
+//                      prefix sum of 1/M; the tail i > b moves by beta.
+//   recompute_pose_graph_orientation (:51-57)  orient_kernel.
+//
+// Rounding: the per-edge residual, d = 2 inv(R^T sigma R) r and the clamp are
+// evaluated like the reference; the range sums use a deterministic block scan
+// instead of the reference's left-to-right loop, so poses agree to rounding
+// (tests: 1e-9 on positions after 20 steps of the reference's lap graph).
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace slamhip {
+
+struct M3 {
+    double a[3][3];
+};
+
+// A @ B with the OpenBLAS dgemm FMA chain (see se2_mul).
+__device__ __forceinline__ M3 m3_mul(const M3& x, const M3& y) {
+    M3 z;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            z.a[i][j] = fma(x.a[i][2], y.a[2][j], fma(x.a[i][1], y.a[1][j], x.a[i][0] * y.a[0][j]));
+    return z;
+}
+
+__device__ __forceinline__ M3 m3_transpose(const M3& x) {
+    M3 z;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) z.a[i][j] = x.a[j][i];
+    return z;
+}
+
+// Inverse by LU with partial pivoting (dgesv on the identity), enough for the
+// well-conditioned R sigma R^T blocks here.
+__device__ __forceinline__ M3 m3_inv(const M3& m) {
+    double A[3][3], X[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            A[i][j] = m.a[i][j];
+            X[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        int p = k;
+        for (int i = k + 1; i < 3; ++i)
+            if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
+        if (p != k) {
+            for (int j = 0; j < 3; ++j) {
+                double t = A[k][j]; A[k][j] = A[p][j]; A[p][j] = t;
+                t = X[k][j]; X[k][j] = X[p][j]; X[p][j] = t;
+            }
+        }
+        for (int i = k + 1; i < 3; ++i) {
+            const double l = A[i][k] / A[k][k];
+            for (int j = k; j < 3; ++j) A[i][j] -= l * A[k][j];
+            for (int j = 0; j < 3; ++j) X[i][j] -= l * X[k][j];
+        }
+    }
+    M3 r;
+    for (int j = 0; j < 3; ++j)
+        for (int i = 2; i >= 0; --i) {
+            double s = X[i][j];
+            for (int k = i + 1; k < 3; ++k) s -= A[i][k] * r.a[k][j];
+            r.a[i][j] = s / A[i][i];
+        }
+    return r;
+}
+
+// construct_R (src/pose_graph_optimization.py:76-85)
+__device__ __forceinline__ M3 rot_z(double theta) {
+    double s, c;
+    sincos(theta, &s, &c);
+    M3 r;
+    r.a[0][0] = c;   r.a[0][1] = -s;  r.a[0][2] = 0.0;
+    r.a[1][0] = s;   r.a[1][1] = c;   r.a[1][2] = 0.0;
+    r.a[2][0] = 0.0; r.a[2][1] = 0.0; r.a[2][2] = 1.0;
+    return r;
+}
+
+__device__ __forceinline__ M3 diag3(double v) {
+    M3 r;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) r.a[i][j] = (i == j) ? v : 0.0;
+    return r;
+}
+
+__device__ __forceinline__ bool is_loop_edge(int a, int b) { return a - b != 1 && b - a != 1; }
+
+// NumPy float remainder (npy_divmod): fmod, then shift into the divisor's sign.
+__device__ __forceinline__ double py_mod(double x, double m) {
+    double r = fmod(x, m);
+    if (r != 0.0) {
+        if ((m < 0.0) != (r < 0.0)) r += m;
+    } else {
+        r = copysign(0.0, m);
+    }
+    return r;
+}
+
+// diag(inv(R sigma R^T)) of edge e (pass 1), 3 doubles per edge.
+__global__ void sgd_dw_kernel(const double* __restrict__ poses, const int32_t* __restrict__ ea,
+                              const int32_t* __restrict__ eb, int32_t E, double sigma,
+                              double* __restrict__ dw) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const M3 R = rot_z(poses[3 * ea[e] + 2]);
+    const M3 W = m3_inv(m3_mul(m3_mul(R, diag3(sigma)), m3_transpose(R)));
+    dw[3 * e + 0] = W.a[0][0];
+    dw[3 * e + 1] = W.a[1][1];
+    dw[3 * e + 2] = W.a[2][2];
+}
+
+// gamma: first edge (networkx order) whose diag(W) has the smallest squared
+// norm, among edges that touch at least one node (a < b).  One wave.
+__global__ void sgd_gamma_kernel(const int32_t* __restrict__ ea, const int32_t* __restrict__ eb,
+                                 int32_t E, const double* __restrict__ dw, double* __restrict__ gamma) {
+    double bestv = INFINITY;
+    int bestj = -1;
+    for (int e = threadIdx.x; e < E; e += 64) {
+        const int a = ea[e], b = eb[e];
+        if (!is_loop_edge(a, b) || a >= b) continue;
+        const double* w = dw + 3 * e;
+        const double n2 = fma(w[2], w[2], fma(w[1], w[1], w[0] * w[0]));
+        if (n2 < bestv) { bestv = n2; bestj = e; }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double ov = __shfl_xor(bestv, off, 64);
+        const int oj = __shfl_xor(bestj, off, 64);
+        if (ov < bestv || (ov == bestv && oj >= 0 && (bestj < 0 || oj < bestj))) { bestv = ov; bestj = oj; }
+    }
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < 3; ++j) gamma[j] = bestj >= 0 ? dw[3 * bestj + j] : INFINITY;
+    }
+}
+
+// M[i][j] in edge order; also 1/M for the relaxation pass.  One thread / node.
+__global__ void sgd_weights_kernel(int32_t N, const int32_t* __restrict__ ea,
+                                   const int32_t* __restrict__ eb, int32_t E,
+                                   const double* __restrict__ dw, double* __restrict__ invM) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    for (int e = 0; e < E; ++e) {
+        const int a = ea[e], b = eb[e];
+        if (!is_loop_edge(a, b)) continue;
+        if (a < i && i <= b) {
+            m0 = m0 + dw[3 * e + 0];
+            m1 = m1 + dw[3 * e + 1];
+            m2 = m2 + dw[3 * e + 2];
+        }
+    }
+    invM[3 * i + 0] = 1.0 / m0;
+    invM[3 * i + 1] = 1.0 / m1;
+    invM[3 * i + 2] = 1.0 / m2;
+}
+
+constexpr int kRelaxBlock = 512;
+
+// Pass 2: one workgroup, sequential over edges.  Poses live in LDS when they
+// fit (N <= kLdsPoses), otherwise in global memory (one CU: workgroup-scope
+// barriers order them).
+constexpr int kLdsPoses = 6144;
+
+template <bool IN_LDS>
+__global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
+    double* __restrict__ g_poses, int32_t N, const int32_t* __restrict__ ea,
+    const int32_t* __restrict__ eb, const double* __restrict__ tf, int32_t E,
+    const double* __restrict__ invM, const double* __restrict__ gamma, double lr, double sigma) {
+    constexpr int WAVES = kRelaxBlock / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* scan_red = reinterpret_cast<double*>(smem);           // WAVES * 3
+    double* P = IN_LDS ? scan_red + WAVES * 4 : g_poses;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+
+    if (IN_LDS) {
+        for (int i = tid; i < 3 * N; i += kRelaxBlock) P[i] = g_poses[i];
+    }
+    __syncthreads();
+
+    const double TWO_PI = 2.0 * M_PI;
+    double alpha[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        alpha[j] = 1.0 / gamma[j];
+        alpha[j] *= lr;
+    }
+    const M3 S = diag3(sigma);
+
+    for (int e = 0; e < E; ++e) {
+        const int a = ea[e], b = eb[e];
+        if (!is_loop_edge(a, b) || a >= b) continue;   // a >= b: the reference's no-op
+
+        // ---- residual (src/pose_graph_optimization.py:29-34), uniform -----------
+        const double pax = P[3 * a], pay = P[3 * a + 1], pat = P[3 * a + 2];
+        const double pbx = P[3 * b], pby = P[3 * b + 1], pbt = P[3 * b + 2];
+        const M3 R = rot_z(pat);                  // construct_R(pg, a)
+        M3 Pa = R;                                // utils.pose_to_mat(poses[a])
+        Pa.a[0][2] = pax;
+        Pa.a[1][2] = pay;
+        M3 Z;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Z.a[k / 3][k % 3] = tf[9 * static_cast<int64_t>(e) + k];
+        const M3 Pb = m3_mul(Pa, Z);
+        double r[3];
+        r[0] = Pb.a[0][2] - pbx;
+        r[1] = Pb.a[1][2] - pby;
+        r[2] = py_mod(atan2(Pb.a[1][0], Pb.a[0][0]) - pbt, TWO_PI);
+        const M3 Wi = m3_inv(m3_mul(m3_mul(m3_transpose(R), S), R));
+        double d[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const M3& w = Wi;
+            d[j] = fma(2.0 * w.a[j][2], r[2], fma(2.0 * w.a[j][1], r[1], (2.0 * w.a[j][0]) * r[0]));
+        }
+
+        // ---- prefix of 1/M over (a, b]: chunked block scan (3 columns) ------------
+        const int L = b - a;
+        const int chunk = (L + kRelaxBlock - 1) / kRelaxBlock;
+        const int lo = a + 1 + tid * chunk;
+        const int hi = min(lo + chunk, b + 1);
+        double loc[3] = {0.0, 0.0, 0.0};
+        for (int i = lo; i < hi; ++i) {
+            loc[0] += invM[3 * i + 0];
+            loc[1] += invM[3 * i + 1];
+            loc[2] += invM[3 * i + 2];
+        }
+        // inclusive wave scan of thread totals (Hillis-Steele, fixed order)
+        double inc[3] = {loc[0], loc[1], loc[2]};
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const double o = __shfl_up(inc[j], off, 64);
+                if (lane >= off) inc[j] = o + inc[j];
+            }
+        }
+        if (lane == 63) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) scan_red[wave * 4 + j] = inc[j];
+        }
+        __syncthreads();
+        double pre[3], tw[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double w0 = 0.0, tot = 0.0;
+            for (int w = 0; w < WAVES; ++w) {
+                const double x = scan_red[w * 4 + j];
+                if (w < wave) w0 += x;
+                tot += x;
+            }
+            pre[j] = w0 + (inc[j] - loc[j]);   // exclusive prefix of this thread
+            tw[j] = tot;                        // total_weight
+        }
+        double beta[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double bj = (static_cast<double>(L) * d[j]) * alpha[j];
+            if (fabs(bj) > fabs(r[j])) bj = r[j];
+            beta[j] = bj;
+        }
+        // ---- apply: i in (a, b] ramps, i > b shifts by the full beta -------------
+        {
+            double run[3] = {pre[0], pre[1], pre[2]};
+            for (int i = lo; i < hi; ++i) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    run[j] += invM[3 * i + j];
+                    P[3 * i + j] += beta[j] * (run[j] / tw[j]);
+                }
+            }
+        }
+        for (int i = b + 1 + tid; i < N; i += kRelaxBlock) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
+        }
+        __syncthreads();
+    }
+    if (IN_LDS) {
+        for (int i = tid; i < 3 * N; i += kRelaxBlock) g_poses[i] = P[i];
+    }
+}
+
+// First loop of recompute_pose_graph_orientation: theta_i from the unit
+// direction to the next pose, i = 1 .. N-2.  Reads columns 0-1, writes 2.
+__global__ void orient_kernel(double* __restrict__ poses, int32_t N) {
+    const int i = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N - 1) return;
+    double vx = poses[3 * (i + 1)] - poses[3 * i];
+    double vy = poses[3 * (i + 1) + 1] - poses[3 * i + 1];
+    const double n = sqrt(fma(vy, vy, vx * vx));
+    if (n > 0.0) {
+        vx = vx / n;
+        vy = vy / n;
+        poses[3 * i + 2] = atan2(vy, vx);
+    }
+}
+
+// Second half of recompute_pose_graph_orientation (:68-74) with icp_recompute:
+// the reverse-order loop theta_i = theta_{i-1} + atan2(T_i[1,0], T_i[0,0])
+// reads theta_{i-1} BEFORE its own update, so every node is independent.
+// tf holds the N-1 rotation-only ICP results of pairs (i, i-1), i = 1..N-1.
+__global__ void copy_theta_kernel(const double* __restrict__ poses, int32_t N, double* __restrict__ th) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) th[i] = poses[3 * i + 2];
+}
+
+__global__ void apply_theta_kernel(double* __restrict__ poses, int32_t N, const double* __restrict__ th,
+                                   const double* __restrict__ tf) {
+    const int i = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double* t = tf + 9 * static_cast<int64_t>(i - 1);
+    poses[3 * i + 2] = th[i - 1] + atan2(t[3], t[0]);
+}
+
+}  // namespace slamhip
+
+using namespace slamhip;
+
+extern "C" {
+
+int64_t slam_pgo_sgd_work_size(int32_t N, int32_t E) {
+    return 3 * static_cast<int64_t>(N) + 3 * static_cast<int64_t>(E) + 4;
+}
+
+int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb,
+                          const double* tf, int32_t E, double learning_rate,
+                          double loop_closure_uncertainty, double* work, void* stream) {
+    if (N < 0 || E < 0) return fail(SLAM_EINVAL, "sgd: N=%d E=%d", N, E);
+    if (N == 0 || E == 0) return ok();
+    if (!poses || !ea || !eb || !tf || !work) return fail(SLAM_EINVAL, "sgd: null array argument");
+    hipStream_t s = as_stream(stream);
+    double* invM = work;
+    double* dw = work + 3 * static_cast<int64_t>(N);
+    double* gamma = dw + 3 * static_cast<int64_t>(E);
+    hipLaunchKernelGGL(sgd_dw_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, E,
+                       loop_closure_uncertainty, dw);
+    hipLaunchKernelGGL(sgd_gamma_kernel, dim3(1), dim3(64), 0, s, ea, eb, E, dw, gamma);
+    hipLaunchKernelGGL(sgd_weights_kernel, dim3((N + 127) / 128), dim3(128), 0, s, N, ea, eb, E, dw,
+                       invM);
+    const size_t red = 4 * (kRelaxBlock / 64) * sizeof(double);
+    if (N <= kLdsPoses) {
+        const size_t lds = red + 3 * static_cast<size_t>(N) * sizeof(double);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxBlock), lds, s, poses, N, ea, eb, tf,
+                           E, invM, gamma, learning_rate, loop_closure_uncertainty);
+    } else {
+        hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxBlock), red, s, poses, N, ea,
+                           eb, tf, E, invM, gamma, learning_rate, loop_closure_uncertainty);
+    }
+    return check_launch("pgo sgd kernels");
+}
+
+// Second half of recompute_pose_graph_orientation (:68-74) with icp_recompute:
+// the reverse-order loop theta_i = theta_{i-1} + atan2(T_i[1,0], T_i[0,0])
+// reads theta_{i-1} BEFORE its own update, so every node is independent once
+// the old thetas are snapshotted (work: N doubles).
+int slam_pgo_orient_from_tf_f64(double* poses, int32_t N, const double* tf, double* work, void* stream) {
+    if (N < 2) return ok();
+    if (!poses || !tf || !work) return fail(SLAM_EINVAL, "orient_from_tf: null array");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(copy_theta_kernel, dim3((N + 255) / 256), dim3(256), 0, s, poses, N, work);
+    hipLaunchKernelGGL(apply_theta_kernel, dim3((N - 1 + 255) / 256), dim3(256), 0, s, poses, N, work, tf);
+    return check_launch("pgo orient_from_tf kernels");
+}
+
+int slam_pgo_orient_f64(double* poses, int32_t N, void* stream) {
+    if (N < 3) return ok();
+    if (!poses) return fail(SLAM_EINVAL, "orient: null poses");
+    hipLaunchKernelGGL(orient_kernel, dim3((N - 2 + 255) / 256), dim3(256), 0, as_stream(stream), poses, N);
+    return check_launch("pgo orient kernel");
+}
+
+}  // extern "C"

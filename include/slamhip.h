@@ -1,0 +1,127 @@
+/*
+ * slamhip.h — C-ABI of the MI355X-native ICP + SE(2) pose-graph hot path.
+ *
+ * Drop-in boundary for cohnt/ICP-SLAM-with-Loop-Closure (reference at
+ * /root/reference).  The reference is pure Python/NumPy, so its "FFI" for this
+ * path is the Python call surface of src/icp.py and
+ * src/pose_graph_optimization.py; the build's drop-in modules
+ * (the .py modules in icp-slam-with-loop-closure_amd/src) bind these entry points with
+ * ctypes.  Each entry point names the reference
+ * function(s) it replaces.
+ *
+ * Conventions (all entry points):
+ *   - every array argument is a DEVICE pointer (hipMalloc / torch-ROCm
+ *     storage) owned by the caller; scalars are host values;
+ *   - points are packed (x, y) float64 pairs ("double2"); the homogeneous
+ *     coordinate of the reference's (n, 3) arrays is implicit and must be 1
+ *     (np.c_[points, ones] as scripts/main.py:242-243 builds them);
+ *   - 3x3 SE(2) matrices are 9 float64, row-major, last row [0, 0, 1];
+ *   - launches are asynchronous and ordered on `stream` (a hipStream_t; NULL
+ *     = the legacy default stream); nothing is allocated, nothing is copied to
+ *     the host, so every call can be captured into a hipGraph;
+ *   - return 0 on success, a negative SLAM_E* code on failure; the message is
+ *     available from slam_last_error() (thread-local).
+ */
+#ifndef SLAMHIP_H
+#define SLAMHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLAM_OK 0
+#define SLAM_EINVAL (-1)   /* bad shape / argument */
+#define SLAM_EHIP (-2)     /* HIP runtime error (launch, device) */
+#define SLAM_ETOOBIG (-3)  /* a scan larger than the compiled query capacity */
+
+/* Library identity: ABI version (major*100 + minor). */
+int slam_abi_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* slam_last_error(void);
+/* Largest query scan (pc1) one workgroup can hold (points). */
+int slam_icp_max_query_points(void);
+
+/*
+ * Batched ICP, one scan pair per workgroup, all iterations on chip.
+ * Replaces src/icp.py:72-97 `icp(pc1, pc2, init_transform, epsilon,
+ * max_iters, stopping_thresh, rotation_only)` for B independent pairs, i.e.
+ * the joblib fan-out of scripts/main.py:240-247,
+ * src/pose_graph_optimization.py:59-68 and src/loop_closure_detection.py:134-142.
+ *
+ *   pts       all scans, packed double2, scan s = pts[scan_off[s] .. scan_off[s+1])
+ *   scan_off  int64[n_scans + 1]
+ *   src_scan  int32[B]  pc1 (moving/query cloud) of pair b
+ *   dst_scan  int32[B]  pc2 (reference cloud) of pair b
+ *   init      float64[B][9] initial transforms
+ *   max_n1/max_n2  host upper bounds of the pc1 / pc2 sizes in this batch
+ *                  (select the kernel instance and LDS size; not checked
+ *                  against the data beyond n1 <= slam_icp_max_query_points())
+ *   hist_stride    0, or >= max_iters + 3: out_hist[b] holds the full
+ *                  transform list [init, T1, ..., T_k] the reference returns
+ *   out_hist  float64[B][hist_stride][9] (NULL if hist_stride == 0)
+ *   out_tf    float64[B][9]  final transform (transforms[-1])
+ *   out_err   float64[B]     returned error (of the penultimate transform)
+ *   out_iters int32[B]       number of ICP iterations k (len(transforms) - 1)
+ * Stopping rules are the reference's: err < epsilon; iteration > max_iters;
+ * |last_err - err| < stopping_thresh from the second iteration on.
+ */
+int slam_icp_batch_f64(const double* pts, const int64_t* scan_off,
+                       const int32_t* src_scan, const int32_t* dst_scan,
+                       const double* init, int32_t B,
+                       double epsilon, int32_t max_iters, double stopping_thresh,
+                       int32_t rotation_only, int32_t max_n1, int32_t max_n2,
+                       int32_t hist_stride, double* out_hist, double* out_tf,
+                       double* out_err, int32_t* out_iters, void* stream);
+
+/*
+ * One ICP iteration per pair.  Replaces src/icp.py:55-69 `icp_iteration(pc1,
+ * pc2, previous_transform, rotation_only)`; with T_in = identity it is
+ * src/icp.py:10-19 `get_correspondences(pc1, pc2)` (an identity transform
+ * reproduces the query coordinates exactly).
+ *   T_in      float64[B][9]
+ *   T_out     float64[B][9]   transform @ previous_transform
+ *   out_corr  int64[...]      correspondences of pair b written at
+ *                             out_corr[corr_off[b] + i], i < n1(b)
+ *   corr_off  int64[B]
+ *   out_err   float64[B]      get_error of the pre-update cloud
+ */
+int slam_icp_step_f64(const double* pts, const int64_t* scan_off,
+                      const int32_t* src_scan, const int32_t* dst_scan,
+                      const double* T_in, int32_t B, int32_t rotation_only,
+                      int32_t max_n1, int32_t max_n2, double* T_out,
+                      int64_t* out_corr, const int64_t* corr_off,
+                      double* out_err, void* stream);
+
+/*
+ * Rigid 2-D fit of matched rows a[i] -> b[i] (n rows each, double2).
+ * Replaces src/icp.py:22-46 `get_transform(pc1, pc2)` (out_T) and
+ * src/icp.py:49-52 `get_error(pc1, pc2)` (out_err, the SUM of squares).
+ */
+int slam_kabsch2d_f64(const double* a, const double* b, int64_t n,
+                      double* out_T, double* out_err, void* stream);
+
+/*
+ * One stochastic-gradient relaxation step, in place on poses (N x 3).
+ * Replaces src/pose_graph_optimization.py:7-49
+ * `pose_graph_optimization_step_sgd(pose_graph, learning_rate,
+ * loop_closure_uncertainty)`.  Edges (ea[e] -> eb[e], tf[e] 3x3) must be in
+ * the pose graph's networkx iteration order; |a-b| == 1 edges are skipped as
+ * in the reference.  `work` is float64[7 * N] device scratch.
+ */
+int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea,
+                          const int32_t* eb, const double* tf, int32_t E,
+                          double learning_rate, double loop_closure_uncertainty,
+                          double* work, void* stream);
+
+/*
+ * Heading recompute from positions, in place.  Replaces the first loop of
+ * src/pose_graph_optimization.py:51-57 `recompute_pose_graph_orientation`.
+ */
+int slam_pgo_orient_f64(double* poses, int32_t N, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAMHIP_H */

@@ -1,0 +1,206 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE.
+
+Runs only in the build container, where the read-only reference lives at
+/root/reference (``src.icp``, ``src.utils``, ``src.pose_graph``
+and ``src.pose_graph_optimization`` import cleanly).  The reference never
+travels to the GPU box; only the .npz/.txt outputs written here do.
+
+    python tests/golden/gen_golden.py
+
+Fixtures (all inputs + reference outputs; no reference code):
+  icp_unit.npz     get_correspondences / get_transform / get_error /
+                   icp_iteration on 4 clouds (n1 != n2 included)
+  icp_cases.npz    icp() on 12 synthetic pairs: main.py params, icp()
+                   defaults, rotation_only, forced max_iters, identity init
+                   with a large offset, ragged pairs
+  sgd.npz          pose_graph_optimization_step_sgd on the seeded
+                   scripts/test_pose_graph_optimization.py lap graph:
+                   1/5/20 steps, flip-every-5 run, orientation recompute
+                   (with and without the rotation-only ICP re-run)
+  posegraph.npz / posegraph_5node.g2o   PoseGraph ctor / flip / g2o export
+"""
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+sys.path.insert(0, REF)
+
+import src.icp as ref_icp  # noqa: E402  (the reference)
+import src.pose_graph as ref_pg  # noqa: E402
+import src.pose_graph_optimization as ref_pgo  # noqa: E402
+import src.utils as ref_utils  # noqa: E402
+from slamhip import synthetic  # noqa: E402
+
+assert ref_icp.__file__.startswith(REF), ref_icp.__file__
+
+
+def pack_list(arrs):
+    off = np.zeros(len(arrs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(a) for a in arrs])
+    return np.concatenate(arrs, axis=0), off
+
+
+def gen_icp_unit():
+    rng = np.random.default_rng(11)
+    out = {}
+    sizes = [(50, 50), (97, 64), (64, 131), (300, 257)]
+    for k, (n1, n2) in enumerate(sizes):
+        pc2 = np.c_[rng.uniform(-5, 5, size=(n2, 2)), np.ones(n2)]
+        th = rng.uniform(-0.3, 0.3)
+        T = ref_utils.pose_to_mat([rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), th])
+        src_idx = rng.integers(0, n2, size=n1)
+        pc1 = np.c_[pc2[src_idx, :2] + rng.normal(0, 0.05, size=(n1, 2)), np.ones(n1)]
+        if k == 3:  # exact duplicate candidates: first-index tie rule of np.argmin
+            pc2[5] = pc2[17]
+            pc2[200] = pc2[17]
+        init = ref_utils.pose_to_mat([0.05, -0.02, 0.01])
+        corr = ref_icp.get_correspondences(pc1, pc2)
+        tf = ref_icp.get_transform(pc1, pc2[corr])
+        err = ref_icp.get_error(pc1, pc2[corr])
+        T1, corr1, err1 = ref_icp.icp_iteration(pc1, pc2, init.copy())
+        out.update({f"pc1_{k}": pc1, f"pc2_{k}": pc2, f"init_{k}": init,
+                    f"corr_{k}": corr.astype(np.int64), f"tf_{k}": tf, f"err_{k}": np.float64(err),
+                    f"it_T_{k}": T1, f"it_corr_{k}": corr1.astype(np.int64), f"it_err_{k}": np.float64(err1)})
+    out["n_cases"] = np.int64(len(sizes))
+    np.savez_compressed(os.path.join(HERE, "icp_unit.npz"), **out)
+
+
+def gen_icp_cases():
+    seq = synthetic.make_sequence(40, seed=0)
+    small = synthetic.make_sequence(40, seed=3, n_beams=361)
+    cases = []
+    # (pc1 scan, pc2 scan, init, epsilon, max_iters, stopping_thresh, rotation_only, label)
+    for i in (1, 7, 19, 33):   # scripts/main.py:241-247 parameters
+        cases.append((seq.scans[i], seq.scans[i - 1],
+                      ref_utils.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]), 0.05, 100, 1e-4, False, "main"))
+    for i in (5, 12):         # icp() defaults
+        cases.append((seq.scans[i], seq.scans[i - 1], np.eye(3), 0.01, 100, 1e-4, False, "defaults"))
+    # rotation-only re-run of src/pose_graph_optimization.py:59-68
+    for i in (9, 25):
+        cases.append((seq.scans[i], seq.scans[i - 1],
+                      ref_utils.pose_to_mat(seq.truth[i] - seq.truth[i - 1]), 0.05, 100, 1e-4, True, "rotation_only"))
+    # forced max_iters (max_iters=3 -> 5 iterations) with a tiny stopping threshold
+    cases.append((seq.scans[15], seq.scans[10], np.eye(3), 1e-9, 3, 1e-15, False, "max_iters"))
+    # identity init with a large offset (loop-closure style, scripts/main.py:302-305)
+    cases.append((seq.scans[30], seq.scans[24], np.eye(3), 0.05, 100, 1e-4, False, "far"))
+    # ragged pairs (n1 != n2), smaller scans
+    a = small.scans[8][::2]
+    b = small.scans[7]
+    cases.append((a, b, ref_utils.pose_to_mat(small.odometry[8] - small.odometry[7]), 0.05, 100, 1e-4, False, "ragged"))
+    cases.append((small.scans[20], small.scans[19][:250], np.eye(3), 0.05, 100, 1e-4, False, "ragged2"))
+
+    pc1s, pc2s, hist, hist_off, out = [], [], [], [0], {}
+    inits, params, errs, n_iter, corr0, labels, init_after = [], [], [], [], [], [], []
+    for (s1, s2, init, eps, mi, st, ro, lab) in cases:
+        pc1 = synthetic.homogeneous(s1)
+        pc2 = synthetic.homogeneous(s2)
+        init_in = np.array(init, dtype=np.float64)
+        init_ref = init_in.copy()
+        tfs, err = ref_icp.icp(pc1, pc2, init_transform=init_ref, epsilon=eps, max_iters=mi,
+                               stopping_thresh=st, rotation_only=ro)
+        assert tfs[0] is init_ref
+        _, c0, _ = ref_icp.icp_iteration(pc1, pc2, init_in.copy(), rotation_only=ro)
+        pc1s.append(s1)
+        pc2s.append(s2)
+        inits.append(init_in)
+        init_after.append(init_ref)   # the reference mutates it when rotation_only
+        params.append([eps, mi, st, float(ro)])
+        errs.append(float(err))
+        n_iter.append(len(tfs) - 1)
+        hist.append(np.stack(tfs))
+        hist_off.append(hist_off[-1] + len(tfs))
+        corr0.append(c0.astype(np.int64))
+        labels.append(lab)
+    out["pc1"], out["off1"] = pack_list(pc1s)
+    out["pc2"], out["off2"] = pack_list(pc2s)
+    out["init"] = np.stack(inits)
+    out["init_after"] = np.stack(init_after)
+    out["params"] = np.array(params)
+    out["err"] = np.array(errs)
+    out["n_iter"] = np.array(n_iter, dtype=np.int64)
+    out["hist"] = np.concatenate(hist)
+    out["hist_off"] = np.array(hist_off, dtype=np.int64)
+    out["corr0"], out["corr0_off"] = np.concatenate(corr0), pack_list(corr0)[1]
+    out["labels"] = np.array(labels)
+    np.savez_compressed(os.path.join(HERE, "icp_cases.npz"), **out)
+    print("icp iterations per case:", n_iter)
+
+
+def edges_of(pg):
+    ea, eb, tf = [], [], []
+    for a, b, t in pg.graph.edges(data="object"):
+        ea.append(a)
+        eb.append(b)
+        tf.append(np.asarray(t, dtype=np.float64))
+    return np.array(ea, dtype=np.int64), np.array(eb, dtype=np.int64), np.stack(tf)
+
+
+def gen_sgd():
+    poses, loops = synthetic.lap_pose_graph(seed=0)
+    out = {"poses0": poses.copy()}
+    pg = ref_pg.PoseGraph(poses.copy())
+    for a, b in loops:
+        pg.add_constraint(a, b, np.eye(3))
+    out["ea"], out["eb"], out["tf"] = edges_of(pg)
+    for k in range(20):
+        ref_pgo.pose_graph_optimization_step_sgd(pg, learning_rate=1 / float(k + 1))
+        if k + 1 in (1, 5, 20):
+            out[f"poses_step{k + 1}"] = pg.poses.copy()
+    ref_pgo.recompute_pose_graph_orientation(pg, None, 100, 0.05, 1, icp_recompute=False)
+    out["poses_recomputed"] = pg.poses.copy()
+
+    # flip every 5 steps, default lr (scripts/test_pose_graph_optimization.py:77-81)
+    pg = ref_pg.PoseGraph(poses.copy())
+    for a, b in loops:
+        pg.add_constraint(a, b, np.eye(3))
+    for it in range(1, 11):
+        if it % 5 == 0:
+            pg.flip()
+        ref_pgo.pose_graph_optimization_step_sgd(pg)
+    out["poses_flip10"] = pg.poses.copy()
+    out["flip_ea"], out["flip_eb"], out["flip_tf"] = edges_of(pg)
+
+    # orientation recompute with the rotation-only ICP re-run on a small sequence
+    seq = synthetic.make_sequence(12, seed=5, n_beams=181)
+    pg = ref_pg.PoseGraph(seq.truth.copy() + np.array([0.01, -0.01, 0.02]))
+    ref_pgo.recompute_pose_graph_orientation(pg, seq.scans, 100, 0.05, 1, icp_recompute=True)
+    scans, off = pack_list(seq.scans)
+    out.update({"rc_poses0": seq.truth.copy() + np.array([0.01, -0.01, 0.02]), "rc_scans": scans,
+                "rc_off": off, "rc_poses": pg.poses.copy()})
+    np.savez_compressed(os.path.join(HERE, "sgd.npz"), **out)
+
+
+def gen_posegraph():
+    odometry = np.array([[0, 0, 0], [1, 0, 0], [2, 0, 0], [2, 1, np.pi / 2], [2, 2, np.pi / 2]], dtype=np.float64)
+    pg = ref_pg.PoseGraph(odometry.copy())
+    pg.add_constraint(0, 4, np.eye(3))
+    out = {"odometry": odometry}
+    out["ea"], out["eb"], out["tf"] = edges_of(pg)
+    with tempfile.TemporaryDirectory() as d:
+        pg.export_g2o(os.path.join(d, "g.g2o"))
+        with open(os.path.join(d, "g.g2o")) as f:
+            g2o = f.read()
+    with open(os.path.join(HERE, "posegraph_5node.g2o"), "w") as f:
+        f.write(g2o)
+    pg.add_constraint(0, 4, ref_utils.pose_to_mat([0.1, 0.2, 0.3]))   # overwrite keeps nx position
+    out["ow_ea"], out["ow_eb"], out["ow_tf"] = edges_of(pg)
+    pg.flip()
+    out["flip_poses"] = pg.poses.copy()
+    out["flip_ea"], out["flip_eb"], out["flip_tf"] = edges_of(pg)
+    np.savez_compressed(os.path.join(HERE, "posegraph.npz"), **out)
+
+
+if __name__ == "__main__":
+    gen_icp_unit()
+    gen_icp_cases()
+    gen_sgd()
+    gen_posegraph()
+    for f in sorted(os.listdir(HERE)):
+        print(f, os.path.getsize(os.path.join(HERE, f)))

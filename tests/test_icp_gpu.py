@@ -1,0 +1,177 @@
+"""GPU parity of the HIP ICP path against the reference (golden fixtures) and
+the CPU oracle, through the C-ABI (slamhip) and the drop-in ``src.icp``.
+
+Tolerances (north star: poses within 1e-5 of the CPU reference):
+  * correspondences: bit-identical (exact fp64 distance, first-min rule);
+  * transforms: |dT| <= 1e-9 (closed-form 2x2 Kabsch + tree reductions vs
+    LAPACK SVD + NumPy summation order);
+  * iteration counts: identical.
+"""
+import numpy as np
+import pytest
+
+from conftest import case_arrays, homog
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def icp():
+    import src.icp as m
+    return m
+
+
+@pytest.fixture(scope="module")
+def k():
+    from slamhip import icp as kk
+    return kk
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    import icp_oracle
+    return icp_oracle
+
+
+def test_unit_vectors(golden, icp):
+    u = golden("icp_unit.npz")
+    for c in range(int(u["n_cases"])):
+        pc1, pc2 = u[f"pc1_{c}"], u[f"pc2_{c}"]
+        corr = icp.get_correspondences(pc1, pc2)
+        assert np.array_equal(corr, u[f"corr_{c}"]), c
+        assert np.allclose(icp.get_transform(pc1, pc2[corr]), u[f"tf_{c}"], rtol=0, atol=1e-12)
+        e = icp.get_error(pc1, pc2[corr])
+        assert abs(e - u[f"err_{c}"]) <= 1e-12 * max(1.0, abs(u[f"err_{c}"]))
+        T, c1, e1 = icp.icp_iteration(pc1, pc2, u[f"init_{c}"].copy())
+        assert np.array_equal(c1, u[f"it_corr_{c}"])
+        assert np.allclose(T, u[f"it_T_{c}"], rtol=0, atol=1e-12)
+        assert abs(e1 - u[f"it_err_{c}"]) <= 1e-12 * max(1.0, abs(u[f"it_err_{c}"]))
+        assert icp.get_closest_point(pc1[3], pc2) == u[f"corr_{c}"][3]
+
+
+def test_tie_first_index(golden, icp):
+    u = golden("icp_unit.npz")
+    pc2 = u["pc2_3"]          # rows 5, 17, 200 are identical
+    assert icp.get_closest_point(pc2[17], pc2) == 5
+    assert icp.get_closest_point(pc2[200], pc2) == 5
+
+
+@pytest.mark.parametrize("c", range(12))
+def test_icp_golden_cases(golden, icp, c):
+    g = golden("icp_cases.npz")
+    pc1, pc2, init, eps, mi, st, ro, hist, err = case_arrays(g, c)
+    tfs, e = icp.icp(pc1, pc2, init, epsilon=eps, max_iters=mi, stopping_thresh=st, rotation_only=ro)
+    assert tfs[0] is init
+    assert np.array_equal(init, g["init_after"][c])        # in-place mutation semantics
+    assert len(tfs) == len(hist), (len(tfs), len(hist))   # same number of iterations
+    assert np.allclose(np.stack(tfs), hist, rtol=0, atol=TOL)
+    assert isinstance(e, np.float64)
+    assert abs(e - err) <= TOL * max(1.0, abs(err))
+
+
+def test_first_iteration_correspondences(golden, icp):
+    g = golden("icp_cases.npz")
+    for c in range(len(g["err"])):
+        pc1, pc2, init, *_ , ro = case_arrays(g, c)[:7]
+        _, corr, _ = icp.icp_iteration(pc1, pc2, g["init"][c].copy(), rotation_only=ro)
+        c0 = g["corr0"][g["corr0_off"][c]:g["corr0_off"][c + 1]]
+        assert np.array_equal(corr, c0), c
+
+
+def _sequence_pairs(n, seed, n_beams=1081):
+    from slamhip import se2, synthetic
+    seq = synthetic.make_sequence(n + 1, seed=seed, n_beams=n_beams)
+    inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, n + 1)])
+    return seq, inits
+
+
+def test_batched_sequence_vs_oracle(k, oracle):
+    """scripts/main.py:240-256 on a 48-pair synthetic stream (config C2 shape)."""
+    n = 48
+    seq, inits = _sequence_pairs(n, seed=1)
+    res = k.icp_batch(seq.scans, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
+    for b in range(0, n, 6):   # oracle on every 6th pair keeps the test fast
+        h, e = oracle.icp(homog(seq.scans[b + 1]), homog(seq.scans[b]), inits[b].copy(), 0.05, 100)
+        assert res.iters[b] == len(h) - 1, b
+        assert np.allclose(res.tf[b], h[-1], rtol=0, atol=TOL)
+        assert abs(res.err[b] - e) <= TOL * max(1.0, e)
+    # odometry chain (a8) matches the reference composition
+    from slamhip import se2
+    chain = se2.compose_chain(seq.odometry[0], res.tf)
+    assert chain.shape == (n + 1, 3)
+    assert np.abs(chain[:, :2] - seq.truth[:, :2] - (seq.odometry[0, :2] - seq.truth[0, :2])).max() < 0.5
+
+
+def test_batch_is_order_independent_and_deterministic(k):
+    n = 40
+    seq, inits = _sequence_pairs(n, seed=7, n_beams=361)
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    r1 = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
+    r2 = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
+    assert np.array_equal(r1.tf, r2.tf) and np.array_equal(r1.err, r2.err)
+    perm = np.random.default_rng(0).permutation(n)
+    r3 = k.icp_batch(seq.scans, src[perm], dst[perm], inits[perm], epsilon=0.05, max_iters=100)
+    assert np.array_equal(r3.tf, r1.tf[perm]) and np.array_equal(r3.iters, r1.iters[perm])
+
+
+def test_every_instance_agrees(k, oracle):
+    """All compiled (BLOCK, QPT) shapes that fit the scan give the same answer."""
+    import ctypes
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 6
+    seq, inits = _sequence_pairs(n, seed=11, n_beams=301)
+    ref = [oracle.icp(homog(seq.scans[b + 1]), homog(seq.scans[b]), inits[b].copy(), 0.05, 100)
+           for b in range(n)]
+    bl, q = ctypes.c_int32(), ctypes.c_int32()
+    try:
+        for i in range(lib.slam_icp_num_instances()):
+            lib.slam_icp_instance_shape(i, ctypes.byref(bl), ctypes.byref(q))
+            if bl.value * q.value < 301:
+                continue
+            lib.slam_icp_force_instance(i)
+            res = k.icp_batch(seq.scans, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
+            for b in range(n):
+                assert res.iters[b] == len(ref[b][0]) - 1, (i, b)
+                assert np.allclose(res.tf[b], ref[b][0][-1], rtol=0, atol=TOL), (i, b)
+    finally:
+        lib.slam_icp_force_instance(-1)
+
+
+def test_large_ragged_scans_tile_path(k, oracle):
+    """pc2 larger than the LDS-resident capacity (4096 points) and a pc1 that
+    needs the 512x16 instance: exercises the streamed-tile path."""
+    rng = np.random.default_rng(3)
+    n2, n1 = 5000, 4500
+    pc2 = rng.uniform(-10, 10, size=(n2, 2))
+    th = 0.02
+    R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    pc1 = (pc2[rng.choice(n2, n1, replace=False)] - [0.05, 0.02]) @ R.T + rng.normal(0, 0.003, (n1, 2))
+    init = np.eye(3)
+    res = k.icp_batch([pc1, pc2], [0], [1], init[None], epsilon=1e-9, max_iters=3, stopping_thresh=1e-15)
+    h, e = oracle.icp(homog(pc1), homog(pc2), init.copy(), 1e-9, 3, 1e-15)
+    assert res.iters[0] == len(h) - 1 == 5
+    assert np.allclose(res.tf[0], h[-1], rtol=0, atol=TOL)
+    _, corr, _ = k.icp_step([pc1, pc2], [0], [1], np.eye(3)[None])
+    assert np.array_equal(corr[0], oracle.correspondences(homog(pc1), homog(pc2)))
+
+
+def test_exact_recovery_and_identity(k):
+    from slamhip import se2
+    rng = np.random.default_rng(5)
+    pc = rng.uniform(-5, 5, size=(700, 2))
+    res = k.icp_batch([pc, pc], [0], [1], np.eye(3)[None], epsilon=1e-30, max_iters=5, history=True)
+    assert res.err[0] == 0.0 and np.allclose(res.tf[0], np.eye(3), atol=1e-15)
+    T = se2.pose_to_mat([0.01, -0.02, 0.003])
+    pc2 = (T[:2, :2] @ pc.T).T + T[:2, 2]
+    res = k.icp_batch([pc, pc2], [0], [1], np.eye(3)[None], epsilon=1e-20, max_iters=50, stopping_thresh=0)
+    assert np.allclose(res.tf[0], T, atol=1e-12)
+
+
+def test_bad_inputs_raise(icp):
+    pc = np.c_[np.zeros((4, 2)), np.full(4, 2.0)]
+    with pytest.raises(ValueError):
+        icp.get_correspondences(pc, pc)
+    with pytest.raises(ValueError):
+        icp.icp(np.zeros((0, 3)), np.ones((3, 3)))

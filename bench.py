@@ -31,9 +31,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
 
 FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (spec), MI355X_MICROARCH.md
+FP32_VALU_PEAK_TFLOPS = 157.3    # MI355X vector FP32 (spec)
 HBM_PEAK_GBPS = 8000.0
-ISSUE_BOUND_EVALS = 256 * 2.4e9 * 64 / 8   # ~8 VALU issue slots per candidate
-FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add (exact NumPy order)
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9          # wave64 VALU op = 2 cycles on a SIMD-32
+INSTR_PER_EVAL = {"screen": 4.5, "exact": 9.0}  # VALU instructions per candidate
+FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add: the reference's work per candidate
 
 
 def log(*a):
@@ -50,7 +52,7 @@ def parse():
     p.add_argument("--strong", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pgo", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=48, help="pairs in the CPU baseline sample")
+    p.add_argument("--cpu-sample", type=int, default=64, help="pairs in the CPU baseline sample")
     p.add_argument("--cpu-workers", type=int, default=16)
     p.add_argument("--instance", type=int, default=-1, help="force a kernel instance (diagnostics)")
     return p.parse_args()
@@ -162,20 +164,31 @@ def main():
     lib = _abi.lib()
     if args.instance >= 0:
         lib.slam_icp_force_instance(args.instance)
+    lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "1")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)
     gathered = None
+    Bpad = max(B, 1)
     if world > 1:
-        gathered = torch.empty((world, max(B, 1), 11), dtype=torch.float64, device=ss.device)
+        if args.strong:
+            Bpad = max((args.pairs + world - 1) // world, 1)
+        gathered = torch.empty((world, Bpad, 11), dtype=torch.float64, device=ss.device)
+        local_res = torch.zeros((Bpad, 11), dtype=torch.float64, device=ss.device)
 
     stream = torch.cuda.current_stream()
+
+    def pack_results(buf):
+        # SE(2) edges + error + iteration count of every pair, padded to Bpad rows
+        if B:
+            buf[:B, :9] = batch.out_tf[:B]
+            buf[:B, 9] = batch.out_err[:B]
+            buf[:B, 10] = batch.out_iters[:B].to(torch.float64)
 
     def step():
         batch.launch()
         if world > 1:
             # SE(2) edges + error + iteration count of every pair -> every rank
-            local_res = torch.cat([batch.out_tf[:max(B, 1)], batch.out_err[:max(B, 1)].unsqueeze(1),
-                                   batch.out_iters[:max(B, 1)].to(torch.float64).unsqueeze(1)], dim=1)
+            pack_results(local_res)
             dist.all_gather_into_tensor(gathered, local_res)
 
     for _ in range(args.warmup):
@@ -191,8 +204,7 @@ def main():
         batch.launch()
         ev[i][1].record(stream)
         if world > 1:
-            local_res = torch.cat([batch.out_tf[:max(B, 1)], batch.out_err[:max(B, 1)].unsqueeze(1),
-                                   batch.out_iters[:max(B, 1)].to(torch.float64).unsqueeze(1)], dim=1)
+            pack_results(local_res)
             dist.all_gather_into_tensor(gathered, local_res)
     torch.cuda.synchronize()
     if world > 1:
@@ -220,7 +232,10 @@ def main():
     ms_per_step = dt_max / args.steps * 1e3
     value = pairs_all * args.steps / dt_max
     # dominant kernel: slam_icp_batch_f64 on rank 0 (its own pairs)
+    screen = os.environ.get("SLAMHIP_SCREEN", "1") != "0" and int(ss.lens.max()) <= 4096
+    peak = FP32_VALU_PEAK_TFLOPS if screen else FP64_VALU_PEAK_TFLOPS
     flops = FLOP_PER_EVAL * evals / (kern_ms * 1e-3) / 1e12
+    issue_bound = VALU_LANE_OPS / INSTR_PER_EVAL["screen" if screen else "exact"]
     alg_bytes = 16.0 * float(ss.lens.sum()) + B * (4 + 4 + 72 + 72 + 8 + 4) + 8 * (len(ss.lens) + 1)
     hbm_gbps = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
@@ -254,15 +269,16 @@ def main():
                    "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}"},
         "roofline": {
             "bound": "valu",
-            "kernel": "slam_icp_batch_f64 (icp_kernel)",
+            "kernel": "slam_icp_batch_f64 (icp_kernel, %s)" % ("fp32 screen + exact fp64 certification"
+                                                               if screen else "exact fp64 scan"),
             "achieved": round(flops, 3),
-            "peak": FP64_VALU_PEAK_TFLOPS,
+            "peak": peak,
             "unit": "TFLOP/s",
-            "frac": round(flops / FP64_VALU_PEAK_TFLOPS, 4),
+            "frac": round(flops / peak, 4),
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 4),
             "candidate_evals_per_launch": evals,
-            "issue_bound_frac": round(evals / (kern_ms * 1e-3) / ISSUE_BOUND_EVALS, 4),
+            "issue_bound_frac": round(evals / (kern_ms * 1e-3) / issue_bound, 4),
             "hbm": {"achieved": round(hbm_gbps, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 6), "algorithmic_bytes_per_launch": alg_bytes},
         },

@@ -33,8 +33,8 @@
 
 namespace slamhip {
 
-constexpr int kCandCap = 4096;        // pc2 points resident in LDS (64 KiB)
-constexpr int kRedDoubles = 2 * 8 * 9;  // two reduction slabs, <= 8 waves x 9
+constexpr int kCandCap = 4096;          // pc2 points resident in LDS (64 KiB fp64 + 32 KiB fp32)
+constexpr int kRedDoubles = 2 * 8 * 9;   // two reduction slabs, <= 8 waves x 9
 
 struct IcpArgs {
     const double2* pts;
@@ -57,21 +57,26 @@ struct IcpArgs {
     const int64_t* corr_off;
 };
 
+// Squared distance with NumPy's rounding: sum((pc2[j] - q)**2) over x, y (+0).
+__device__ __forceinline__ double exact_d2(double px, double py, double qx, double qy) {
+    const double dx = px - qx;
+    const double dy = py - qy;
+    return dx * dx + dy * dy;   // -ffp-contract=off: two roundings, then the add
+}
+
 // Exhaustive first-minimum nearest neighbour of QPT queries per lane against
-// `cnt` candidates in LDS (all lanes read the same candidate: broadcast).
+// `cnt` fp64 candidates in LDS (all lanes read the same candidate: broadcast).
 template <int QPT>
-__device__ __forceinline__ void nn_scan(const double2* __restrict__ cand, int cnt, int base,
-                                        const double (&qx)[QPT], const double (&qy)[QPT],
-                                        double (&best)[QPT], int (&bi)[QPT]) {
+__device__ __forceinline__ void nn_scan_f64(const double2* __restrict__ cand, int cnt, int base,
+                                            const double (&qx)[QPT], const double (&qy)[QPT],
+                                            double (&best)[QPT], int (&bi)[QPT]) {
 #pragma unroll 2
     for (int j = 0; j < cnt; ++j) {
         const double2 p = cand[j];
         const int jj = base + j;
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
-            const double dx = p.x - qx[k];
-            const double dy = p.y - qy[k];
-            const double d = dx * dx + dy * dy;   // NumPy: sum((pc - point)**2, axis=1)
+            const double d = exact_d2(p.x, p.y, qx[k], qy[k]);
             const bool lt = d < best[k];
             best[k] = lt ? d : best[k];
             bi[k] = lt ? jj : bi[k];
@@ -79,16 +84,77 @@ __device__ __forceinline__ void nn_scan(const double2* __restrict__ cand, int cn
     }
 }
 
-template <int BLOCK, int QPT, bool STEP>
+// fp32 screen, chunked: candidates are visited in chunks of kChunk; per
+// query only the chunk minimum is tracked inside a chunk (4 fp32 ops + half a
+// v_min3 per candidate), and across chunks the smallest chunk minimum (M1, in
+// chunk C1) and the second smallest (M2).  The winning chunk is re-scanned
+// afterwards for the index and the in-chunk runner-up.  Candidates are padded
+// to a multiple of kChunk with far sentinels (d32 = +inf).
+constexpr int kChunk = 32;
+constexpr float kSentinel = 3.0e19f;
+
+__device__ __forceinline__ float screen_d32(float px, float py, float qx, float qy) {
+    const float dx = px - qx;
+    const float dy = py - qy;
+    return fmaf(dy, dy, dx * dx);
+}
+
+template <int QPT>
+__device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf, int n_pad,
+                                                const float (&qx)[QPT], const float (&qy)[QPT],
+                                                float (&M1)[QPT], float (&M2)[QPT], int (&C1)[QPT]) {
+    for (int c0 = 0; c0 < n_pad; c0 += kChunk) {
+        float cm[QPT];
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) cm[k] = INFINITY;
+#pragma unroll 4
+        for (int j = c0; j < c0 + kChunk; ++j) {
+            const float2 p = candf[j];
+#pragma unroll
+            for (int k = 0; k < QPT; ++k) cm[k] = fminf(cm[k], screen_d32(p.x, p.y, qx[k], qy[k]));
+        }
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const bool lt = cm[k] < M1[k];
+            M2[k] = __builtin_amdgcn_fmed3f(M1[k], M2[k], cm[k]);   // M1 <= M2
+            C1[k] = lt ? c0 : C1[k];
+            M1[k] = fminf(M1[k], cm[k]);
+        }
+    }
+}
+
+// Lower bound of the exact squared distance T of any candidate whose fp32
+// screened distance is >= d32 (DESIGN.md §"fp32 screen, exact answer"):
+// d32 <= F(T) = (1+8u) T + 3a sqrt(T) + 3a^2 with u = 2^-24 and a the
+// coordinate-rounding bound (1+u) u (|p|max + |q|max); T >= F^{-1}(d32).
+__device__ __forceinline__ double screen_lower_bound(double d32, double a) {
+    const double alpha = 1.0 + 8.0 * 0x1p-24;
+    const double beta = 3.0 * a;
+    const double gamma = 3.0 * a * a + 1e-37;
+    const double disc = beta * beta - 4.0 * alpha * (gamma - d32);
+    if (!(disc > 0.0)) return 0.0;
+    const double s = (-beta + sqrt(disc)) / (2.0 * alpha);
+    if (!(s > 0.0)) return 0.0;
+    return s * s * (1.0 - 1e-12);
+}
+
+template <int BLOCK, int QPT, bool STEP, bool SCREEN>
 __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* red0 = reinterpret_cast<double*>(smem);
     double* red1 = red0 + WAVES * 8;
     double2* cand = reinterpret_cast<double2*>(smem + kRedDoubles * sizeof(double));
+    const int cap = a.cand_cap;
+    // SCREEN only: fp32 copy of the candidates and per-wave fallback queues
+    float2* candf = reinterpret_cast<float2*>(cand + cap);
+    int* fq = reinterpret_cast<int*>(candf + cap);          // [WAVES][64*QPT] query ids
+    int* fres = fq + WAVES * 64 * QPT;                       // [WAVES][64*QPT] exact answers
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int s1 = a.src_scan[b];
     const int s2 = a.dst_scan[b];
     const int64_t o1 = a.scan_off[s1];
@@ -97,12 +163,37 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
     const double2* __restrict__ p1 = a.pts + o1;
     const double2* __restrict__ p2 = a.pts + o2;
-    const int cap = a.cand_cap;
     const bool resident = n2 <= cap;
 
+    double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound)
     if (resident) {
-        for (int j = tid; j < n2; j += BLOCK) cand[j] = p2[j];
+        for (int j = tid; j < n2; j += BLOCK) {
+            const double2 p = p2[j];
+            cand[j] = p;
+            if constexpr (SCREEN) {
+                candf[j] = make_float2(static_cast<float>(p.x), static_cast<float>(p.y));
+                cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
+            }
+        }
+        if constexpr (SCREEN) {
+            for (int j = n2 + tid; j < (n2 + kChunk - 1) / kChunk * kChunk; j += BLOCK)
+                candf[j] = make_float2(kSentinel, kSentinel);
+        }
     }
+    bool screen = false;
+    if constexpr (SCREEN) {
+        double cm[1] = {cmax};
+        // block max through the sum slab: max is exact, order-free
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) cm[0] = fmax(cm[0], __shfl_xor(cm[0], off, 64));
+        if (lane == 0) red1[wave] = cm[0];
+        __syncthreads();
+        cmax = red1[0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) cmax = fmax(cmax, red1[w]);
+        screen = cmax < 1e18;   // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
+    }
+    const int n2_pad = (n2 + kChunk - 1) / kChunk * kChunk;
 
     SE2 T = load_se2(a.init + 9 * static_cast<int64_t>(b));
     if (a.rotation_only) {   // src/icp.py:60-61 zeroes previous_transform[:2, 2]
@@ -117,34 +208,137 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
 
     double last_err = 0.0;
     for (int it = 0;; ++it) {
-        // ---- src/icp.py:62  pc1_transformed = T @ pc1 -------------------------
-        double qx[QPT], qy[QPT], best[QPT];
+        double qx[QPT], qy[QPT];
         int bi[QPT];
+        if constexpr (SCREEN) {
+            // ---- fp32 screen over LDS-resident candidates ---------------------
+            {
+                float fx[QPT], fy[QPT], M1[QPT], M2[QPT];
+                int C1[QPT];
 #pragma unroll
-        for (int k = 0; k < QPT; ++k) {
-            const int i = k * BLOCK + tid;
-            double x = 0.0, y = 0.0;
-            if (i < n1) {
-                const double2 p = p1[i];
-                x = p.x;
-                y = p.y;
+                for (int k = 0; k < QPT; ++k) {
+                    const int i = k * BLOCK + tid;
+                    double x = 0.0, y = 0.0;
+                    if (i < n1) {
+                        const double2 p = p1[i];
+                        x = p.x;
+                        y = p.y;
+                    }
+                    const double tx = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));
+                    const double ty = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+                    fx[k] = static_cast<float>(tx);
+                    fy[k] = static_cast<float>(ty);
+                    M1[k] = INFINITY;
+                    M2[k] = INFINITY;
+                    C1[k] = 0;
+                }
+                if (screen) nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
+                // ---- certify: the screened winner is the exact fp64 argmin? ---
+                int base = 0;
+#pragma unroll
+                for (int k = 0; k < QPT; ++k) {
+                    const int i = k * BLOCK + tid;
+                    double x = 0.0, y = 0.0;
+                    if (i < n1) {
+                        const double2 p = p1[i];
+                        x = p.x;
+                        y = p.y;
+                    }
+                    qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));   // bit-identical to above
+                    qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+                    // winning chunk: first index reaching the chunk minimum + runner-up
+                    float b1 = INFINITY, b2 = INFINITY;
+                    int j1 = C1[k];
+#pragma unroll 2
+                    for (int j = C1[k]; j < C1[k] + kChunk; ++j) {
+                        const float2 p = candf[j];
+                        const float d = screen_d32(p.x, p.y, fx[k], fy[k]);
+                        b2 = __builtin_amdgcn_fmed3f(b1, b2, d);
+                        if (d < b1) j1 = j;
+                        b1 = fminf(b1, d);
+                    }
+                    j1 = min(j1, n2 - 1);
+                    bi[k] = j1;
+                    bool ok = true;
+                    if (!screen) {
+                        ok = i >= n1;   // |coordinates| >= 1e18: every query takes the exact path
+                    } else if (i < n1 && n2 > 1) {
+                        const double2 c = cand[j1];
+                        const double d1 = exact_d2(c.x, c.y, qx[k], qy[k]);
+                        const double s2 = static_cast<double>(fminf(M2[k], b2));   // every other j: d32 >= s2
+                        const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
+                        const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
+                        ok = cq < 1e18 && s2 < 3.0e38 && screen_lower_bound(s2, ab) > d1;
+                    }
+                    const uint64_t fails = __ballot(!ok);
+                    if (!ok) {
+                        const int pos = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                            static_cast<uint32_t>(fails >> 32),
+                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(fails), 0u)));
+                        fq[wave * 64 * QPT + pos] = i;
+                        bi[k] = -1 - pos;   // resolved below
+                    }
+                    base += __popcll(fails);
+                }
+                // ---- wave-cooperative exact fallback for uncertified queries ---
+                for (int t = 0; t < base; ++t) {
+                    const int i = fq[wave * 64 * QPT + t];
+                    const double2 p = p1[i];
+                    const double x = fma(T.m02, 1.0, fma(T.m01, p.y, T.m00 * p.x));
+                    const double y = fma(T.m12, 1.0, fma(T.m11, p.y, T.m10 * p.x));
+                    double bd = INFINITY;
+                    int bj = lane < n2 ? lane : 0x7fffffff;
+                    for (int j = lane; j < n2; j += 64) {
+                        const double2 c = cand[j];
+                        const double d = exact_d2(c.x, c.y, x, y);
+                        if (d < bd) {
+                            bd = d;
+                            bj = j;
+                        }
+                    }
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) {
+                        const double od = __shfl_xor(bd, off, 64);
+                        const int oj = __shfl_xor(bj, off, 64);
+                        if (od < bd || (od == bd && oj < bj)) {
+                            bd = od;
+                            bj = oj;
+                        }
+                    }
+                    if (lane == 0) fres[wave * 64 * QPT + t] = bj;
+                }
             }
-            qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));
-            qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
-            best[k] = INFINITY;
-            bi[k] = 0;
-        }
-
-        // ---- src/icp.py:63  correspondences (exhaustive NN) -------------------
-        if (resident) {
-            nn_scan<QPT>(cand, n2, 0, qx, qy, best, bi);
+            __syncthreads();   // fres visible to every lane of the wave
+#pragma unroll
+            for (int k = 0; k < QPT; ++k)
+                if (bi[k] < 0) bi[k] = fres[wave * 64 * QPT + (-1 - bi[k])];
         } else {
-            for (int t0 = 0; t0 < n2; t0 += cap) {
-                const int cnt = min(cap, n2 - t0);
-                __syncthreads();
-                for (int j = tid; j < cnt; j += BLOCK) cand[j] = p2[t0 + j];
-                __syncthreads();
-                nn_scan<QPT>(cand, cnt, t0, qx, qy, best, bi);
+            // ---- exact fp64 scan (src/icp.py:62-63) ---------------------------
+            double best[QPT];
+#pragma unroll
+            for (int k = 0; k < QPT; ++k) {
+                const int i = k * BLOCK + tid;
+                double x = 0.0, y = 0.0;
+                if (i < n1) {
+                    const double2 p = p1[i];
+                    x = p.x;
+                    y = p.y;
+                }
+                qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));
+                qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+                best[k] = INFINITY;
+                bi[k] = 0;
+            }
+            if (resident) {
+                nn_scan_f64<QPT>(cand, n2, 0, qx, qy, best, bi);
+            } else {
+                for (int t0 = 0; t0 < n2; t0 += cap) {
+                    const int cnt = min(cap, n2 - t0);
+                    __syncthreads();
+                    for (int j = tid; j < cnt; j += BLOCK) cand[j] = p2[t0 + j];
+                    __syncthreads();
+                    nn_scan_f64<QPT>(cand, cnt, t0, qx, qy, best, bi);
+                }
             }
         }
 
@@ -164,7 +358,7 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                 v[1] += qy[k];
                 v[2] += m.x;
                 v[3] += m.y;
-                v[4] += best[k];   // == (pc1_t - pc2[corr])**2 summed over the row
+                v[4] += exact_d2(m.x, m.y, qx[k], qy[k]);   // (pc1_t - pc2[corr])**2 of the row
             }
         }
         block_sum<5, WAVES>(v, red0);
@@ -249,31 +443,50 @@ using KernelFn = void (*)(IcpArgs);
 struct Instance {
     int block;
     int qpt;
-    KernelFn batch;
+    KernelFn batch;          // exact fp64 scan
     KernelFn step;
+    KernelFn batch_screen;   // fp32 screen + exact certification
+    KernelFn step_screen;
 };
 
-#define SLAM_INST(B, Q) {B, Q, icp_kernel<B, Q, false>, icp_kernel<B, Q, true>}
+#define SLAM_INST(B, Q)                                                                   \
+    {B, Q, icp_kernel<B, Q, false, false>, icp_kernel<B, Q, true, false>,                 \
+     icp_kernel<B, Q, false, true>, icp_kernel<B, Q, true, true>}
 static const Instance kInstances[] = {
-    SLAM_INST(64, 1),   SLAM_INST(64, 2),   SLAM_INST(64, 4),   SLAM_INST(64, 8),
-    SLAM_INST(64, 12),  SLAM_INST(64, 17),  SLAM_INST(128, 9),  SLAM_INST(128, 12),
-    SLAM_INST(128, 16), SLAM_INST(256, 5),  SLAM_INST(256, 8),  SLAM_INST(256, 12),
-    SLAM_INST(256, 16), SLAM_INST(512, 16),
+    SLAM_INST(64, 1),   SLAM_INST(64, 2),   SLAM_INST(64, 4),   SLAM_INST(128, 3),
+    SLAM_INST(128, 4),  SLAM_INST(192, 4),  SLAM_INST(192, 6),  SLAM_INST(256, 4),
+    SLAM_INST(256, 5),  SLAM_INST(320, 4),  SLAM_INST(384, 3),  SLAM_INST(512, 3),
+    SLAM_INST(576, 2),  SLAM_INST(512, 4),  SLAM_INST(512, 6),  SLAM_INST(512, 8),
+    SLAM_INST(512, 16),
 };
 #undef SLAM_INST
 constexpr int kNumInstances = sizeof(kInstances) / sizeof(kInstances[0]);
 constexpr int kMaxQuery = 512 * 16;
 
+// Relative per-lane throughput of an instance shape, measured on MI355X with
+// the C3 workload (profiles/r01_instance_sweep_*.jsonl): QPT 5-6 at 192-256
+// threads keeps enough waves resident and enough queries per LDS read.
+static double shape_efficiency(int block, int qpt) {
+    static const double by_qpt[17] = {0, 0.50, 0.60, 0.80, 0.90, 1.00, 0.88, 0.70, 0.60,
+                                      0.50, 0.45, 0.45, 0.40, 0.35, 0.35, 0.30, 0.30};
+    double e = by_qpt[qpt < 16 ? qpt : 16];
+    if (block > 384) e *= 0.75;
+    return e;
+}
+
 static const Instance* pick_instance(int max_n1, int forced) {
     if (forced >= 0 && forced < kNumInstances) return &kInstances[forced];
     const Instance* bestp = nullptr;
+    double best_cost = 0.0;
     for (int i = 0; i < kNumInstances; ++i) {
         const Instance& c = kInstances[i];
         const int capq = c.block * c.qpt;
         if (capq < max_n1) continue;
-        if (!bestp) { bestp = &c; continue; }
-        const int bcap = bestp->block * bestp->qpt;
-        if (capq < bcap || (capq == bcap && c.block < bestp->block)) bestp = &c;
+        const double cost = static_cast<double>(capq) / shape_efficiency(c.block, c.qpt);
+        if (!bestp || cost < best_cost) {
+            bestp = &c;
+            best_cost = cost;
+        }
     }
     return bestp;
 }
@@ -325,18 +538,23 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
     }
 }
 
+static int g_screen = 1;
+
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
                   void* stream) {
     const Instance* inst = pick_instance(max_n1, g_forced_instance);
     if (!inst) return fail(SLAM_ETOOBIG, "query scan of %d points exceeds capacity %d", max_n1, kMaxQuery);
     IcpArgs a = args;
-    a.cand_cap = max_n2 < kCandCap ? (max_n2 > 0 ? max_n2 : 1) : kCandCap;
-    const size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
-    KernelFn fn = step ? inst->step : inst->batch;
+    a.cand_cap = max_n2 < kCandCap ? ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk : kCandCap;
+    const bool screen = g_screen && max_n2 <= kCandCap;
+    size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
+    if (screen)
+        lds += static_cast<size_t>(a.cand_cap) * sizeof(float2) +
+               2 * sizeof(int) * static_cast<size_t>(inst->block) * inst->qpt;
+    KernelFn fn = screen ? (step ? inst->step_screen : inst->batch_screen) : (step ? inst->step : inst->batch);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        static_cast<int>(lds));
-    hipLaunchKernelGGL(fn, dim3(B), dim3(inst->block), lds,
-                       as_stream(stream), a);
+                              static_cast<int>(lds));
+    hipLaunchKernelGGL(fn, dim3(B), dim3(inst->block), lds, as_stream(stream), a);
     return check_launch(step ? "icp_step kernel" : "icp_batch kernel");
 }
 
@@ -363,6 +581,10 @@ int slam_icp_instance_shape(int i, int* block, int* qpt) {
 }
 int slam_icp_force_instance(int i) {
     g_forced_instance = (i >= 0 && i < kNumInstances) ? i : -1;
+    return ok();
+}
+int slam_icp_set_screen(int enable) {
+    g_screen = enable ? 1 : 0;
     return ok();
 }
 int slam_icp_selected_instance(int max_n1) {

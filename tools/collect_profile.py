@@ -1,0 +1,47 @@
+"""Copy the judged pieces of a gpurun profiling pass (tools/gpu_profile.sh)
+into profiles/ and derive per-launch HBM traffic for the ICP kernel.
+
+FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half of the
+bytes of wide (16 B/lane) coalesced reads (MI355X_MICROARCH.md §HBM), which is
+the access pattern of every bulk load in icp_kernel, so it is doubled."""
+import csv
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag):
+    src = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "icp_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    vals = {}
+    rows_out = []
+    for name, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+        d = os.path.join(src, sub)
+        f = [x for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
+        for r in csv.DictReader(open(os.path.join(d, f))):
+            if "icp_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name:
+                vals[name] = float(r["Counter_Value"])
+                rows_out.append({k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
+                                                   "VGPR_Count", "SGPR_Count", "Counter_Name", "Counter_Value")})
+    with open(os.path.join(dst, f"{tag}_pmc_icp.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows_out[0]))
+        w.writeheader()
+        w.writerows(rows_out)
+    fetch = vals["FETCH_SIZE"] * 1024 * 2      # gfx950: FETCH_SIZE = 1/2 of wide coalesced reads
+    write = vals["WRITE_SIZE"] * 1024
+    out = {"icp_batch_bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch, "write_bytes": write,
+           "raw_FETCH_SIZE_KiB": vals["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": vals["WRITE_SIZE"],
+           "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one launch",
+           "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
+           "tag": tag}
+    json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round profiling recipe (run on the GPU box from the repo root):
+#   kernel trace + stats of the bench, then FETCH_SIZE and WRITE_SIZE in
+#   separate PMC passes (MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE need
+#   separate passes; FETCH_SIZE under-reports wide coalesced reads by 2x).
+set -e
+TAG=${1:-r01}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o icp -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_traced.json 2> $OUT/bench_traced.err
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o f -- \
+    python3 tools/prof_icp.py 10000 1 > $OUT/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o w -- \
+    python3 tools/prof_icp.py 10000 1 > $OUT/pmc_write.log 2>&1
+find $OUT -name "*.csv" | head -20

@@ -23,6 +23,7 @@ def main():
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, pairs + 1)])
     ss = k.ScanSet(seq.scans)
     lib = _abi.lib()
+    lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "1")))
     b, q = ctypes.c_int32(), ctypes.c_int32()
     rows = []
     for i in [-1] + list(range(lib.slam_icp_num_instances())):

@@ -1,0 +1,156 @@
+"""Gauss-Newton SE(2) pose-graph optimisation on the GPU.
+
+Host side of ``slam_gn_iteration_f64`` (csrc/gn_kernels.hip).  The symbolic
+work is done once per graph STRUCTURE (it does not change across iterations):
+
+1. node ordering: reverse Cuthill-McKee over the node adjacency (SciPy), the
+   gauge node removed; node n owns scalar columns node_col[n] .. +2 of H;
+2. half-bandwidth W (scalars) of H in that order;
+3. H block slots: one per free node (diagonal block) and one per connected
+   free node pair (off-diagonal block of the lower band), each with the list
+   of edge contributions it sums, in edge order (deterministic assembly).
+
+Everything per iteration runs on the device: linearisation, assembly, band
+Cholesky, substitution, pose update.  Problem definition (residual, Jacobians,
+information 2 I / 5 I as src/pose_graph.py:61-73 exports them) is documented
+in csrc/gn_kernels.hip and oracle/gn_oracle.py.
+"""
+import time
+
+import numpy as np
+import scipy.sparse as sp
+from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+from . import _abi
+from . import device as dv
+
+ODOM_INFO = 2.0
+LOOP_INFO = 5.0
+
+
+class GnPlan:
+    """Symbolic analysis of one graph structure."""
+
+    def __init__(self, N, ea, eb, fixed=0):
+        ea = np.asarray(ea, dtype=np.int64)
+        eb = np.asarray(eb, dtype=np.int64)
+        self.N = N
+        self.fixed = fixed
+        adj = sp.coo_matrix((np.ones(2 * len(ea) + N), (np.r_[ea, eb, np.arange(N)], np.r_[eb, ea, np.arange(N)])),
+                            shape=(N, N)).tocsr()
+        order = reverse_cuthill_mckee(adj, symmetric_mode=True)
+        order = order[order != fixed]
+        node_col = np.full(N, -1, dtype=np.int32)
+        node_col[order] = 3 * np.arange(len(order), dtype=np.int32)
+        self.node_col = node_col
+        self.nv = 3 * len(order)
+        ca, cb = node_col[ea], node_col[eb]
+        both = (ca >= 0) & (cb >= 0)
+        self.W = int(max(2, (np.abs(ca[both] - cb[both]).max() + 2) if both.any() else 2))
+
+        # diagonal slots: free node n, items 2e + side
+        diag_items = [[] for _ in range(N)]
+        pair_items = {}
+        for e in range(len(ea)):
+            a, b = int(ea[e]), int(eb[e])
+            if a == b:
+                continue   # a self-loop has zero Jacobian sum: no H contribution
+            if node_col[a] >= 0:
+                diag_items[a].append(2 * e)
+            if node_col[b] >= 0:
+                diag_items[b].append(2 * e + 1)
+            if node_col[a] >= 0 and node_col[b] >= 0:
+                row, col = (a, b) if node_col[a] > node_col[b] else (b, a)
+                pair_items.setdefault((row, col), []).append(2 * e + (0 if row == a else 1))
+        rc, ptr, items = [], [0], []
+        for n in order:
+            rc.append((node_col[n], node_col[n]))
+            items.extend(diag_items[n])
+            ptr.append(len(items))
+        for (row, col), its in pair_items.items():
+            rc.append((node_col[row], node_col[col]))
+            items.extend(its)
+            ptr.append(len(items))
+        self.slot_rc = np.asarray(rc, dtype=np.int32).reshape(-1, 2)
+        self.slot_ptr = np.asarray(ptr, dtype=np.int32)
+        self.slot_items = np.asarray(items if items else [0], dtype=np.int32)
+        self.n_slots = len(rc)
+
+
+class GaussNewton:
+    def __init__(self, poses, ea, eb, tf, odom_information=ODOM_INFO, loop_information=LOOP_INFO, fixed=0,
+                 device=None, plan=None):
+        poses = np.ascontiguousarray(poses, dtype=np.float64)
+        ea = np.asarray(ea, dtype=np.int32)
+        eb = np.asarray(eb, dtype=np.int32)
+        self.N, self.E = len(poses), len(ea)
+        self.plan = plan if plan is not None else GnPlan(self.N, ea, eb, fixed)
+        w = np.where(np.abs(eb.astype(np.int64) - ea) == 1, odom_information, loop_information).astype(np.float64)
+        self.poses = dv.to_dev(poses, np.float64, device)
+        dev = self.poses.device
+        self.ea = dv.to_dev(ea, np.int32, dev)
+        self.eb = dv.to_dev(eb, np.int32, dev)
+        self.tf = dv.to_dev(np.asarray(tf, dtype=np.float64).reshape(-1, 9), np.float64, dev)
+        self.w = dv.to_dev(w, np.float64, dev)
+        p = self.plan
+        self.node_col = dv.to_dev(p.node_col, np.int32, dev)
+        self.slot_rc = dv.to_dev(p.slot_rc, np.int32, dev)
+        self.slot_ptr = dv.to_dev(p.slot_ptr, np.int32, dev)
+        self.slot_items = dv.to_dev(p.slot_items, np.int32, dev)
+        n = int(_abi.lib().slam_gn_work_size(self.N, self.E, p.W))
+        self.work = dv.empty((n,), np.float64, dev)
+        self.status = dv.to_dev(np.zeros(1, np.int32), np.int32, dev)
+        self.chi2 = None
+
+    def iterate(self, chi2_out, stream=None):
+        """One asynchronous GN iteration; chi2 (before the step) -> chi2_out (device)."""
+        p = self.plan
+        _abi.check(_abi.lib().slam_gn_iteration_f64(
+            dv.ptr(self.poses), self.N, dv.ptr(self.ea), dv.ptr(self.eb), dv.ptr(self.tf), dv.ptr(self.w), self.E,
+            dv.ptr(self.node_col), dv.ptr(self.slot_rc), dv.ptr(self.slot_ptr), dv.ptr(self.slot_items),
+            p.n_slots, p.nv, p.W, dv.ptr(self.work), dv.ptr(chi2_out), dv.ptr(self.status),
+            dv.stream_handle(stream)), "slam_gn_iteration_f64")
+
+    def run(self, iterations=10, tol=None, stream=None):
+        """Run `iterations` steps; returns the chi2 before every step (host)."""
+        t = dv.torch()
+        chis = t.zeros(max(iterations, 1), dtype=t.float64, device=self.poses.device)
+        for k in range(iterations):
+            self.iterate(chis[k:k + 1], stream)
+        out = chis[:iterations].cpu().numpy()
+        if int(self.status.cpu().numpy()[0]) != 0:
+            raise _abi.SlamHipError("Gauss-Newton: H is not positive definite (disconnected graph?)")
+        self.chi2 = out
+        return out
+
+    def host_poses(self):
+        return self.poses.cpu().numpy().reshape(self.N, 3)
+
+
+def optimize(poses, ea, eb, tf, iterations=10, **kw):
+    s = GaussNewton(poses, ea, eb, tf, **kw)
+    chis = s.run(iterations)
+    return s.host_poses(), chis
+
+
+def bench_c4(iterations=10, reps=3):
+    """GN iterations/s on config C4 (5k nodes / 20k edges), for bench.py."""
+    from . import synthetic
+    t = dv.torch()
+    guess, ea, eb, tf, _ = synthetic.lap_graph_c4()
+    t0 = time.perf_counter()
+    plan = GnPlan(len(guess), ea, eb)
+    plan_s = time.perf_counter() - t0
+    s = GaussNewton(guess, ea, eb, tf, plan=plan)
+    s.run(2)   # warm-up
+    best = None
+    for _ in range(reps):
+        s.poses.copy_(dv.to_dev(guess, np.float64, s.poses.device))
+        t.cuda.synchronize()
+        t0 = time.perf_counter()
+        chis = s.run(iterations)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"gn_iters_per_sec": round(iterations / best, 2), "gn_ms_per_iter": round(best / iterations * 1e3, 4),
+            "gn_graph": f"{len(guess)} nodes / {len(ea)} edges (C4)", "gn_band_W": plan.W,
+            "gn_plan_s": round(plan_s, 3), "gn_chi2_first_last": [float(chis[0]), float(chis[-1])]}

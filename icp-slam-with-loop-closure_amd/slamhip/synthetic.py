@@ -181,3 +181,59 @@ def lap_pose_graph(side_len=3.0, poses_per_side=30, num_loops=4, seed=0,
     edges.append((0, per_lap))
     edges.append((len(poses) - 1, len(poses) - 1 - per_lap))
     return poses, edges
+
+
+def _wrap(a):
+    return a - 2 * np.pi * np.floor((a + np.pi) / (2 * np.pi))
+
+
+def lap_graph_c4(seed=0, poses_per_side=125, num_loops=10, side_len=3.0, n_loops=15001,
+                 odo_xy=0.01, odo_th=0.01):
+    """Config C4: 5,000-node / 20,000-edge SE(2) graph.
+
+    Lap trajectory (side 3 m, 125 poses per side, 10 laps), 4,999 odometry
+    edges with RELATIVE noisy measurements, 15,001 distinct loop edges between
+    the same lap position on distinct laps (exact relative measurement), initial
+    guess = dead reckoning of the odometry.  Returns (guess, ea, eb, tf, truth).
+    """
+    rng = np.random.default_rng(seed)
+    per_lap = 4 * poses_per_side
+    N = per_lap * num_loops
+    step = side_len / poses_per_side
+    truth = np.zeros((N, 3))
+    for i in range(1, N):
+        th = truth[i - 1, 2]
+        truth[i, 0] = truth[i - 1, 0] + step * np.cos(th)
+        truth[i, 1] = truth[i - 1, 1] + step * np.sin(th)
+        truth[i, 2] = th + (np.pi / 2 if i % poses_per_side == 0 else 0.0)
+    truth[:, 2] = _wrap(truth[:, 2])
+
+    def rel(a, b):
+        c, s = np.cos(a[2]), np.sin(a[2])
+        d = b[:2] - a[:2]
+        return np.array([c * d[0] + s * d[1], -s * d[0] + c * d[1], _wrap(b[2] - a[2])])
+
+    def mat(p):
+        c, s = np.cos(p[2]), np.sin(p[2])
+        return np.array([[c, -s, p[0]], [s, c, p[1]], [0, 0, 1.0]])
+
+    ea, eb, tf = [], [], []
+    guess = np.zeros((N, 3))
+    for i in range(N - 1):
+        m = rel(truth[i], truth[i + 1]) + np.array([rng.normal(0, odo_xy), rng.normal(0, odo_xy),
+                                                     rng.normal(0, odo_th)])
+        ea.append(i)
+        eb.append(i + 1)
+        tf.append(mat(m))
+        c, s = np.cos(guess[i, 2]), np.sin(guess[i, 2])
+        guess[i + 1] = [guess[i, 0] + c * m[0] - s * m[1], guess[i, 1] + s * m[0] + c * m[1], _wrap(guess[i, 2] + m[2])]
+    pairs = set()
+    while len(pairs) < n_loops:
+        pos = int(rng.integers(per_lap))
+        l1, l2 = sorted(rng.choice(num_loops, 2, replace=False))
+        pairs.add((pos + per_lap * int(l1), pos + per_lap * int(l2)))
+    for a, b in sorted(pairs):
+        ea.append(a)
+        eb.append(b)
+        tf.append(mat(rel(truth[a], truth[b])))
+    return guess, np.array(ea), np.array(eb), np.stack(tf), truth

@@ -108,18 +108,58 @@ int slam_kabsch2d_f64(const double* a, const double* b, int64_t n,
  * `pose_graph_optimization_step_sgd(pose_graph, learning_rate,
  * loop_closure_uncertainty)`.  Edges (ea[e] -> eb[e], tf[e] 3x3) must be in
  * the pose graph's networkx iteration order; |a-b| == 1 edges are skipped as
- * in the reference.  `work` is float64[7 * N] device scratch.
+ * in the reference.  `work`: float64[slam_pgo_sgd_work_size(N, E)] scratch.
  */
 int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea,
                           const int32_t* eb, const double* tf, int32_t E,
                           double learning_rate, double loop_closure_uncertainty,
                           double* work, void* stream);
 
+/* float64 elements of the `work` scratch slam_pgo_sgd_step_f64 needs. */
+int64_t slam_pgo_sgd_work_size(int32_t N, int32_t E);
+
 /*
  * Heading recompute from positions, in place.  Replaces the first loop of
  * src/pose_graph_optimization.py:51-57 `recompute_pose_graph_orientation`.
  */
 int slam_pgo_orient_f64(double* poses, int32_t N, void* stream);
+
+/*
+ * Second half of recompute_pose_graph_orientation with icp_recompute
+ * (src/pose_graph_optimization.py:68-74): theta_i = theta_{i-1} +
+ * atan2(tf_i[1,0], tf_i[0,0]) for i = 1..N-1, theta_{i-1} taken BEFORE its
+ * own update (the reference's reverse-order loop).  tf: float64[N-1][9]
+ * rotation-only ICP results of pairs (i, i-1); work: float64[N].
+ */
+int slam_pgo_orient_from_tf_f64(double* poses, int32_t N, const double* tf,
+                                double* work, void* stream);
+
+/*
+ * One Gauss-Newton iteration of the SE(2) pose graph (north-star solve; the
+ * reference has only the SGD relaxation).  Problem: the graph as
+ * src/pose_graph.py:61-73 exports it to g2o — edge e: ea[e] -> eb[e] with
+ * relative measurement tf[e] and isotropic information w[e]; node columns
+ * node_col[n] (-1 = fixed) in a bandwidth-reducing order; H lower band of
+ * half-width W scalars; slot_* list the edge contributions of every H block
+ * (see slamhip/gn.py GnPlan).  Poses are updated in place; chi2 before the
+ * step -> *out_chi2 (device); *status != 0 if H was not positive definite.
+ */
+int64_t slam_gn_work_size(int32_t N, int32_t E, int32_t W);
+int slam_gn_max_lds_band(void);
+int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea,
+                          const int32_t* eb, const double* tf, const double* w,
+                          int32_t E, const int32_t* node_col,
+                          const int32_t* slot_rc, const int32_t* slot_ptr,
+                          const int32_t* slot_items, int32_t n_slots,
+                          int32_t nv, int32_t W, double* work,
+                          double* out_chi2, int32_t* status, void* stream);
+
+/* Diagnostics (kernel-shape sweeps; not needed by callers). */
+int slam_icp_num_instances(void);
+int slam_icp_instance_shape(int i, int* block, int* qpt);
+int slam_icp_force_instance(int i);
+int slam_icp_selected_instance(int max_n1);
+int slam_icp_set_screen(int enable);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,7 @@ def declared():
 def test_header_parses():
     names = declared()
     assert "slam_icp_batch_f64" in names and "slam_pgo_sgd_step_f64" in names
+    assert "slam_gn_iteration_f64" in names
 
 
 def test_library_exports_every_declared_symbol():

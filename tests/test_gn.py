@@ -1,0 +1,131 @@
+"""Gauss-Newton pose-graph solve: planner host logic (CPU) and GPU parity
+against the float64 oracle (oracle/gn_oracle.py).
+
+The reference has no GN, so parity is "HIP vs the build's
+own CPU restatement" and is unpinned against the reference; tolerance 1e-8 on
+poses after several iterations (band Cholesky vs SuperLU rounding)."""
+import numpy as np
+import pytest
+
+import gn_oracle as go
+
+
+def _random_graph(N, n_loops, seed):
+    from slamhip import se2
+    rng = np.random.default_rng(seed)
+    truth = np.cumsum(rng.normal(0, [0.3, 0.3, 0.2], size=(N, 3)), axis=0)
+    ea, eb, tf = [], [], []
+
+    def rel(a, b):
+        c, s = np.cos(truth[a, 2]), np.sin(truth[a, 2])
+        d = truth[b, :2] - truth[a, :2]
+        return se2.pose_to_mat([c * d[0] + s * d[1], -s * d[0] + c * d[1], truth[b, 2] - truth[a, 2]])
+
+    for i in range(N - 1):
+        ea.append(i)
+        eb.append(i + 1)
+        tf.append(rel(i, i + 1) @ se2.pose_to_mat(rng.normal(0, [0.02, 0.02, 0.01])))
+    for _ in range(n_loops):
+        a, b = rng.choice(N, 2, replace=False)
+        ea.append(int(a))
+        eb.append(int(b))
+        tf.append(rel(a, b))
+    guess = truth + rng.normal(0, [0.1, 0.1, 0.05], size=(N, 3))
+    guess[0] = truth[0]
+    return guess, np.array(ea), np.array(eb), np.stack(tf)
+
+
+def test_plan_covers_every_edge():
+    from slamhip import gn
+    guess, ea, eb, tf = _random_graph(60, 40, 1)
+    p = gn.GnPlan(len(guess), ea, eb)
+    assert p.nv == 3 * 59 and p.node_col[0] == -1
+    cols = p.node_col
+    assert sorted(cols[cols >= 0]) == list(range(0, p.nv, 3))
+    # every non-self edge appears in the diagonal slots of its free endpoints
+    # and in exactly one pair slot when both are free
+    seen_diag, seen_pair = {}, {}
+    for s in range(p.n_slots):
+        r0, c0 = p.slot_rc[s]
+        for it in p.slot_items[p.slot_ptr[s]:p.slot_ptr[s + 1]]:
+            key = (int(it) >> 1, int(it) & 1)
+            (seen_diag if r0 == c0 else seen_pair)[key] = seen_diag.get(key, 0) + 1
+            assert r0 >= c0 and r0 - c0 <= p.W
+    for e in range(len(ea)):
+        if ea[e] == eb[e]:
+            continue
+        if cols[ea[e]] >= 0:
+            assert (e, 0) in seen_diag
+        if cols[eb[e]] >= 0:
+            assert (e, 1) in seen_diag
+    assert len(seen_pair) == sum(1 for e in range(len(ea)) if cols[ea[e]] >= 0 and cols[eb[e]] >= 0)
+    # bandwidth is tight
+    both = (cols[ea] >= 0) & (cols[eb] >= 0)
+    assert p.W == max(2, np.abs(cols[ea][both] - cols[eb][both]).max() + 2)
+
+
+def test_oracle_converges_on_c4():
+    from slamhip import synthetic
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=25, num_loops=4, n_loops=300)
+    p, chis = go.optimize(guess, ea, eb, tf, iterations=5)
+    assert chis[-1] < 1e-3 * chis[0]
+    assert np.abs(p[:, :2] - truth[:, :2]).max() < 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("iters", [1, 3])
+def test_gn_small_vs_oracle(iters):
+    from slamhip import gn
+    guess, ea, eb, tf = _random_graph(80, 30, 2)
+    ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=iters)
+    got, chi = gn.optimize(guess, ea, eb, tf, iterations=iters)
+    assert np.allclose(chi, ref_chi, rtol=1e-9, atol=1e-9)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
+    assert np.abs(go.wrap(got[:, 2] - ref[:, 2])).max() <= 1e-8
+
+
+@pytest.mark.gpu
+def test_gn_c4_vs_oracle():
+    """Config C4: 5,000 nodes / 20,000 edges, 5 iterations."""
+    from slamhip import gn, synthetic
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
+    ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=5)
+    got, chi = gn.optimize(guess, ea, eb, tf, iterations=5)
+    assert np.allclose(chi, ref_chi, rtol=1e-8)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
+    assert np.abs(go.wrap(got[:, 2] - ref[:, 2])).max() <= 1e-8
+    assert chi[-1] < 1e-3 * chi[0]
+
+
+@pytest.mark.gpu
+def test_gn_wide_band_global_window():
+    """Random long-range loops: the band exceeds the LDS window, exercising the
+    global-memory Cholesky window."""
+    from slamhip import _abi, gn
+    guess, ea, eb, tf = _random_graph(150, 120, 3)
+    plan = gn.GnPlan(len(guess), ea, eb)
+    assert plan.W > _abi.lib().slam_gn_max_lds_band()
+    ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=2)
+    got, chi = gn.optimize(guess, ea, eb, tf, iterations=2)
+    assert np.allclose(chi, ref_chi, rtol=1e-9)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
+
+
+@pytest.mark.gpu
+def test_optimize_pose_graph_dropin():
+    """src.pose_graph_optimization.optimize_pose_graph on a reference-style
+    PoseGraph (odometry edges from PoseGraph.__init__, identity loop edges)."""
+    import src.pose_graph as pgm
+    import src.pose_graph_optimization as pgo
+    from slamhip import synthetic
+    poses, loops = synthetic.lap_pose_graph(seed=0)
+    pg = pgm.PoseGraph(poses.copy())
+    for a, b in loops:
+        pg.add_constraint(a, b, np.eye(3))
+    ea, eb, tf = pg.edge_arrays()
+    ref, ref_chi = go.optimize(poses.copy(), ea, eb, tf, iterations=3)
+    obj = pg.poses
+    chis = pgo.optimize_pose_graph(pg, iterations=3, return_history=True)
+    assert pg.poses is obj
+    assert np.allclose(chis, ref_chi, rtol=1e-8)
+    assert np.abs(pg.poses[:, :2] - ref[:, :2]).max() <= 1e-8

@@ -72,13 +72,17 @@ def init_dist(args):
     return world, rank, local
 
 
+def sd_shard_per(n, world):
+    from slamhip import dist as sd
+    return sd.shard_range(n, world, 0)[2]
+
+
 def make_workload(args, world, rank):
     from slamhip import se2, synthetic
+    from slamhip import dist as sd
     if args.strong:
         total = args.pairs
-        per = (total + world - 1) // world
-        lo = min(rank * per, total)
-        hi = min(lo + per, total)
+        lo, hi, _ = sd.shard_range(total, world, rank)
         seq = synthetic.make_sequence(total + 1, seed=2025, n_beams=args.beams)
         scans = seq.scans[lo:hi + 1]
         odo = seq.odometry[lo:hi + 1]
@@ -171,18 +175,17 @@ def main():
     Bpad = max(B, 1)
     if world > 1:
         if args.strong:
-            Bpad = max((args.pairs + world - 1) // world, 1)
+            Bpad = max(sd_shard_per(args.pairs, world), 1)
         gathered = torch.empty((world, Bpad, 11), dtype=torch.float64, device=ss.device)
         local_res = torch.zeros((Bpad, 11), dtype=torch.float64, device=ss.device)
 
     stream = torch.cuda.current_stream()
 
+    from slamhip import dist as sd
+
     def pack_results(buf):
         # SE(2) edges + error + iteration count of every pair, padded to Bpad rows
-        if B:
-            buf[:B, :9] = batch.out_tf[:B]
-            buf[:B, 9] = batch.out_err[:B]
-            buf[:B, 10] = batch.out_iters[:B].to(torch.float64)
+        sd.pack(batch.out_tf[:B], batch.out_err[:B], batch.out_iters[:B], Bpad, out=buf)
 
     def step():
         batch.launch()

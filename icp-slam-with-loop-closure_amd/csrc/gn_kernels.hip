@@ -20,7 +20,8 @@
 //   gn_factor_kernel      ONE workgroup: blocked right-looking band Cholesky,
 //                         the active (W + S) x (W + S) window resident in LDS,
 //                         L overwrites H in place
-//   gn_solve_kernel       ONE workgroup: blocked forward / backward substitution
+//   gn_factor_kernel also runs the forward substitution; gn_backsolve_kernel
+//                         (ONE workgroup) the backward one from the panel store
 //   gn_update_kernel      x <- x + dx, headings wrapped to [-pi, pi)
 // Band work is latency-bound (a chain of 3 (N-1) / S dependent block steps);
 // the roofline is not the lever at C4 size.
@@ -37,6 +38,14 @@ namespace slamhip {
 constexpr int kGnContrib = 34;   // per-edge: 9 AtWA, 9 AtWB, 9 BtWB, 3 AtWe, 3 BtWe, 1 chi2
 constexpr int kGnBlock = 512;    // threads of the factor / solve workgroup
 constexpr int kGnS = 16;         // Cholesky block size (scalar columns per step)
+
+// Broadcast lane l's double (l wave-uniform) through SGPRs (v_readlane).
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), l);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
 
 __device__ __forceinline__ double wrap_pi(double a) {
     return a - 2.0 * M_PI * floor((a + M_PI) / (2.0 * M_PI));
@@ -147,181 +156,315 @@ __global__ void gn_assemble_kernel(const double* __restrict__ contrib, const int
     }
 }
 
-// Blocked band Cholesky, one workgroup.  Window: rows/cols [k0, k0 + M),
-// M = W + S, stored cyclically (index mod M) in `win` (LDS or global scratch).
-// Only lower-triangle band entries are ever read; every row is zeroed when it
-// enters the window so structural zeros stay zero.
-template <bool LDS_WIN>
-__global__ __launch_bounds__(kGnBlock) void gn_factor_kernel(double* __restrict__ Hb, int32_t nv, int32_t W,
-                                                             double* __restrict__ gwin,
-                                                             int32_t* __restrict__ status) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int M = W + kGnS;
-    double* win = LDS_WIN ? lds : gwin;
-    const int ld = W + 1;
-    const int tid = threadIdx.x;
+// Blocked band Cholesky + forward substitution, one workgroup.
+// Window: rows/cols [k0, k0 + MP), MP a power of two >= W + S, stored
+// cyclically (index & (MP-1)) in `win` (LDS, or global scratch when W is
+// large).  Only lower-triangle band entries are read; a row's slots are zeroed
+// before it enters.  Every finished block column is written to the panel store
+// PS as [S x S diagonal factor | W x S panel] (row-major, fixed stride per
+// step) for the backward sweep, and y = L^-1 rhs overwrites rhs.
+// Per step: (a) wave 0 factors the diagonal block in registers and solves its
+// part of y; (b) one thread per panel row forms L[r][block] and updates y[r];
+// (c) rank-S update of the trailing band from a compact LDS copy of the panel,
+// retiring rows' slots zeroed; (d) entering rows (prefetched at the start of
+// the step) are written.  Three barriers per step.
+constexpr int kGnFBlock = 256;   // factor workgroup: one wave per SIMD -> up to 512 VGPRs, no spills
+constexpr int kGnPf = 11;  // prefetch registers per worker thread: S*MP <= kGnPf*(kGnFBlock-64)
+// Compact panel, TRANSPOSED: LpT[t][i] = L[k0+sb+i][k0+t]; row length lpw(W)
+// (multiple of 4): a lane reading 4 consecutive i is one conflict-free 32-B chunk.
+__host__ __device__ constexpr int lpw(int W) { return ((W + 3) / 4) * 4 + 4; }
 
-    // rows [ra, rb) enter the window: zero their slots, then copy their band
-    auto load_rows = [&](int ra, int rb) {
-        for (int idx = tid; idx < (rb - ra) * M; idx += kGnBlock) win[((ra + idx / M) % M) * M + idx % M] = 0.0;
-        __syncthreads();
-        for (int idx = tid; idx < (rb - ra) * ld; idx += kGnBlock) {
-            const int r = ra + idx / ld, d = idx % ld;
-            if (d <= r) win[(r % M) * M + (r - d) % M] = Hb[static_cast<int64_t>(r) * ld + d];
+template <bool LDS_WIN>
+__global__ __launch_bounds__(kGnFBlock) void gn_factor_kernel(const double* __restrict__ Hb, double* __restrict__ rhs,
+                                                             int32_t nv, int32_t W, int32_t MP,
+                                                             double* __restrict__ gwin, double* __restrict__ gLp,
+                                                             double* __restrict__ PS, int32_t* __restrict__ status,
+                                                             unsigned long long* __restrict__ stamps) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double Ld[kGnS][kGnS + 1];
+    // diagnostic phase timers (thread 0, s_memtime ticks), only when `stamps`
+    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0;
+    auto stamp = [&](int ph) {
+        if (stamps && threadIdx.x == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (ph >= 0) tph[ph] += t - tprev;
+            tprev = t;
         }
     };
-    load_rows(0, min(M, nv));
+    __shared__ double yb[kGnS];
+    __shared__ double rdiag[kGnS];
+    const int mask = MP - 1;
+    const int MS = MP + 1;   // padded row stride: column walks hit distinct LDS banks
+    double* win = LDS_WIN ? lds : gwin;
+    const int LPW = lpw(W);
+    double* Lp = LDS_WIN ? lds + static_cast<size_t>(MP) * MS : gLp;        // [S][LPW] transposed panel
+    double* yw = Lp + static_cast<size_t>(kGnS) * LPW;                       // [MP]
+    const int ld = W + 1;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int64_t ps_stride = static_cast<int64_t>(kGnS + W) * kGnS;
+    auto WIN = [&](int r, int c) -> double& { return win[(r & mask) * MS + (c & mask)]; };
+
+    // initial window: rows [0, min(MP, nv))
+    const int r_init = min(MP, nv);
+    for (int idx = tid; idx < r_init * MS; idx += kGnFBlock) win[idx] = 0.0;
+    __syncthreads();
+    for (int idx = tid; idx < r_init * ld; idx += kGnFBlock) {
+        const int r = idx / ld, d = idx % ld;
+        if (d <= r) WIN(r, r - d) = Hb[static_cast<int64_t>(r) * ld + d];
+    }
+    for (int r = tid; r < r_init; r += kGnFBlock) yw[r & mask] = rhs[r];
     __syncthreads();
 
-    for (int k0 = 0; k0 < nv; k0 += kGnS) {
-        const int sb = min(kGnS, nv - k0);
-        // (a) dense Cholesky of the sb x sb diagonal block by wave 0, rows in registers
-        if (tid < 64) {
-            const int lane = tid;
-            double row[kGnS];
+    const int wave = tid >> 6;
+    constexpr int kWorkers = kGnFBlock - 64;        // waves 1.. : trailing update + entering rows
+    const bool can_pf = kGnS * MP <= kGnPf * kWorkers;
+
+    // Wave 0: factor the sb x sb diagonal block at k0 (lane i holds row i,
+    // column values broadcast with v_readlane) and solve its part of y.
+    auto diag_factor = [&](int k0, int sb, int step) {
+        double* ps = PS + step * ps_stride;
+        double row[kGnS], rdv[kGnS];
 #pragma unroll
-            for (int c = 0; c < kGnS; ++c)
-                row[c] = (lane < sb && c <= lane) ? win[((k0 + lane) % M) * M + (k0 + c) % M] : 0.0;
-            bool bad = false;
+        for (int c = 0; c < kGnS; ++c) {
+            row[c] = (lane < sb && c <= lane) ? WIN(k0 + lane, k0 + c) : 0.0;
+            rdv[c] = 0.0;
+        }
+        bool bad = false;
 #pragma unroll
-            for (int j = 0; j < kGnS; ++j) {
-                if (j < sb) {
-                    const double piv = __shfl(row[j], j, 64);
-                    bad |= !(piv > 0.0);
-                    const double d = sqrt(piv);
-                    if (lane == j) row[j] = d;
-                    if (lane > j) row[j] = row[j] / d;
-                    const double lij = row[j];
+        for (int j = 0; j < kGnS; ++j) {
+            if (j < sb) {
+                const double piv = readlane_d(row[j], j);
+                bad |= !(piv > 0.0);
+                const double rd = rsqrt(piv);
+                const double d = piv * rd;
+                rdv[j] = rd;
+                if (lane == j) row[j] = d;
+                if (lane > j) row[j] = row[j] * rd;
 #pragma unroll
-                    for (int c = j + 1; c < kGnS; ++c) {
-                        const double lcj = __shfl(row[j], c, 64);
-                        if (lane > j && c <= lane) row[c] -= lij * lcj;
-                    }
+                for (int c = j + 1; c < kGnS; ++c) {
+                    const double lcj = readlane_d(row[j], c);
+                    if (lane > j && c <= lane) row[c] = fma(-row[j], lcj, row[c]);
                 }
             }
-            if (lane < sb) {
-#pragma unroll
-                for (int c = 0; c < kGnS; ++c)
-                    if (c <= lane) win[((k0 + lane) % M) * M + (k0 + c) % M] = row[c];
-            }
-            if (bad && lane == 0) *status = 1;
         }
-        __syncthreads();
-        // (b) panel rows r in [k0 + sb, min(nv, k0 + sb + W)): L[r][k0..] = A[r][k0..] L_D^-T
+        double y = lane < sb ? yw[(k0 + lane) & mask] : 0.0;
+#pragma unroll
+        for (int t = 0; t < kGnS; ++t) {
+            if (t < sb) {
+                const double yt = readlane_d(y, t) * rdv[t];
+                if (lane == t) y = yt;
+                if (lane > t) y = fma(-row[t], yt, y);
+            }
+        }
+        if (lane < sb) {
+#pragma unroll
+            for (int c = 0; c < kGnS; ++c) {
+                const double v = c <= lane ? row[c] : 0.0;
+                Ld[lane][c] = v;
+                ps[lane * kGnS + c] = v;
+            }
+            rdiag[lane] = rdv[0];
+#pragma unroll
+            for (int c = 1; c < kGnS; ++c)
+                if (lane == c) rdiag[lane] = rdv[c];
+            yb[lane] = y;
+            rhs[k0 + lane] = y;
+        }
+        if (bad && lane == 0) *status = 1;
+    };
+
+    stamp(-1);
+    if (wave == 0) diag_factor(0, min(kGnS, nv), 0);
+    __syncthreads();
+    stamp(0);
+    for (int k0 = 0, step = 0; k0 < nv; k0 += kGnS, ++step) {
+        const int sb = min(kGnS, nv - k0);
         const int rend = min(nv, k0 + sb + W);
-        for (int r = k0 + sb + tid; r < rend; r += kGnBlock) {
-            double* wr = win + (r % M) * M;
+        const int n = rend - (k0 + sb);
+        double* ps = PS + step * ps_stride;
+        const int k1 = k0 + sb;                       // next block
+        const int sb2 = k1 < nv ? min(kGnS, nv - k1) : 0;
+        // rows entering the window at the end of this step (prefetched by the workers)
+        const int ra = k0 + MP, rb = min(nv, k0 + MP + sb);
+        double pf[kGnPf];
+        if (can_pf && wave > 0) {
+            const int wt = tid - 64;
+#pragma unroll
+            for (int q = 0; q < kGnPf; ++q) {
+                const int idx = wt + q * kWorkers;
+                const int r = ra + idx / MP, d = idx % MP;   // slot of column r - d
+                pf[q] = (r < rb && d <= W && d <= r) ? Hb[static_cast<int64_t>(r) * ld + d] : 0.0;
+            }
+        }
+        // (b) panel rows: L[r][k0+t] = (A[r][k0+t] - sum_q L[r][k0+q] Ld[t][q]) / Ld[t][t]
+        for (int i = tid; i < n; i += kGnFBlock) {
+            asm volatile("" ::: "memory");   // keep the Ld reads inside the loop (no LICM into registers)
+            const int r = k0 + sb + i;
             double l[kGnS];
+            double ydot = 0.0;
 #pragma unroll
             for (int t = 0; t < kGnS; ++t) {
+                double v = 0.0;
                 if (t < sb) {
-                    double v = wr[(k0 + t) % M];
-                    const double* dt = win + ((k0 + t) % M) * M;
+                    v = WIN(r, k0 + t);
 #pragma unroll
-                    for (int q = 0; q < t; ++q) v -= l[q] * dt[(k0 + q) % M];
-                    l[t] = v / dt[(k0 + t) % M];
-                    wr[(k0 + t) % M] = l[t];
+                    for (int q = 0; q < t; ++q) v = fma(-l[q], Ld[t][q], v);
+                    v = v * rdiag[t];
+                    ydot = fma(v, yb[t], ydot);
                 }
+                l[t] = v;
+            }
+#pragma unroll
+            for (int t = 0; t < kGnS; ++t) {
+                Lp[t * LPW + i] = l[t];
+                ps[(kGnS + i) * kGnS + t] = l[t];
+            }
+            yw[r & mask] -= ydot;
+        }
+        __syncthreads();
+        stamp(1);
+        if (wave == 0) {
+            // (c1) look-ahead: update the NEXT diagonal block first, then factor it
+            if (sb2 > 0) {
+                for (int e = lane; e < kGnS * kGnS; e += 64) {
+                    const int i = e >> 4, j = e & (kGnS - 1);
+                    if (i < sb2 && j <= i) {
+                        double acc = 0.0;
+#pragma unroll
+                        for (int t = 0; t < kGnS; ++t) acc = fma(Lp[t * LPW + i], Lp[t * LPW + j], acc);
+                        WIN(k1 + i, k1 + j) -= acc;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                diag_factor(k1, sb2, step + 1);
+            }
+        } else {
+            // (c2) rank-sb update of the rest of the trailing band (panel rows
+            // i >= sb2), 4 x 4 register tiles over the lower triangle
+            const int wt = tid - 64;
+            const int nt = (n + 3) / 4;
+            const int t0 = sb2 / 4;                   // first tile row that has rows >= sb2
+            const int ntiles = nt * (nt + 1) / 2 - t0 * (t0 + 1) / 2;
+            for (int q = wt; q < ntiles; q += kWorkers) {
+                // lower-triangle tile q (rows ti >= t0) -> (ti, tj)
+                const int qq = q + t0 * (t0 + 1) / 2;
+                int ti = static_cast<int>((sqrtf(8.0f * qq + 1.0f) - 1.0f) * 0.5f);
+                while ((ti + 1) * (ti + 2) / 2 <= qq) ++ti;
+                while (ti * (ti + 1) / 2 > qq) --ti;
+                const int tj = qq - ti * (ti + 1) / 2;
+                double acc[4][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
+#pragma unroll 4
+                for (int t = 0; t < kGnS; ++t) {
+                    const double2* row = reinterpret_cast<const double2*>(Lp + t * LPW);
+                    const double2 a0 = row[2 * ti], a1 = row[2 * ti + 1];
+                    const double2 b0 = row[2 * tj], b1 = row[2 * tj + 1];
+                    const double li[4] = {a0.x, a0.y, a1.x, a1.y};
+                    const double lj[4] = {b0.x, b0.y, b1.x, b1.y};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) acc[u][v] = fma(li[u], lj[v], acc[u][v]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int i = 4 * ti + u, j = 4 * tj + v;
+                        if (i < n && i >= sb2 && j <= i) WIN(k1 + i, k1 + j) -= acc[u][v];
+                    }
+            }
+            // rows [ra, rb) enter the slots of the retired rows [k0, k0+sb):
+            // every slot of an entering row is written (band value or 0), so
+            // no separate zeroing pass and no extra barrier are needed
+            if (ra < rb) {
+                if (can_pf) {
+#pragma unroll
+                    for (int q = 0; q < kGnPf; ++q) {
+                        const int idx = wt + q * kWorkers;
+                        const int r = ra + idx / MP, d = idx % MP;
+                        if (r < rb) WIN(r, r - d) = pf[q];
+                    }
+                } else {
+                    for (int idx = wt; idx < (rb - ra) * MP; idx += kWorkers) {
+                        const int r = ra + idx / MP, d = idx % MP;
+                        WIN(r, r - d) = (d <= W && d <= r) ? Hb[static_cast<int64_t>(r) * ld + d] : 0.0;
+                    }
+                }
+                for (int r = ra + wt; r < rb; r += kWorkers) yw[r & mask] = rhs[r];
             }
         }
         __syncthreads();
-        // (c) write the finished block column (diag block + panel) back as L
-        for (int idx = tid; idx < (rend - k0) * sb; idx += kGnBlock) {
-            const int r = k0 + idx / sb, t = idx % sb;
-            const int c = k0 + t;
-            if (c <= r && r - c <= W) Hb[static_cast<int64_t>(r) * ld + (r - c)] = win[(r % M) * M + c % M];
-        }
-        // (d) trailing update of the band below the block: (r, c), k0+sb <= c <= r < rend
-        const int n = rend - (k0 + sb);
-        for (int idx = tid; idx < n * n; idx += kGnBlock) {
-            const int r = k0 + sb + idx / n, c = k0 + sb + idx % n;
-            if (c > r || r - c > W) continue;
-            const double* wr = win + (r % M) * M;
-            const double* wc = win + (c % M) * M;
-            double acc = 0.0;
-#pragma unroll
-            for (int t = 0; t < kGnS; ++t)
-                if (t < sb) acc = fma(wr[(k0 + t) % M], wc[(k0 + t) % M], acc);
-            win[(r % M) * M + c % M] -= acc;
-        }
-        __syncthreads();
-        // (e) rows entering the window take the slots of rows k0 .. k0 + sb
-        if (k0 + M < nv) load_rows(k0 + M, min(nv, k0 + M + sb));
-        __syncthreads();
+        stamp(2);
+        stamp(3);
+    }
+    if (stamps && tid == 0) {
+        for (int q = 0; q < 5; ++q) stamps[q] = tph[q];
     }
 }
 
-// Solve L L^T dx = rhs in place (rhs -> dx), one workgroup, blocks of S rows.
-// x is staged in LDS when it fits (LDS_X); L rows are read contiguously in
-// both sweeps (the backward sweep is column-oriented: each finished block
-// subtracts its contribution from the rows above).
+// Backward substitution L^T x = y (y in x on entry), one workgroup, block
+// steps in reverse, reading the panel store PS contiguously; the next step's
+// block is prefetched into registers while the current one is reduced.
 template <bool LDS_X>
-__global__ __launch_bounds__(kGnBlock) void gn_solve_kernel(const double* __restrict__ Lb, int32_t nv, int32_t W,
-                                                            double* __restrict__ gx) {
+__global__ __launch_bounds__(kGnBlock) void gn_backsolve_kernel(const double* __restrict__ PS, int32_t nv, int32_t W,
+                                                                double* __restrict__ gx) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    __shared__ double blk[kGnS][kGnS + 1];
+    __shared__ double part[kGnBlock / 64][kGnS];
     double* x = LDS_X ? lds : gx;
-    const int ld = W + 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int WAVES = kGnBlock / 64;
+    const int t = tid & (kGnS - 1);       // column of the block
+    const int g = tid / kGnS;             // row group
+    constexpr int G = kGnBlock / kGnS;    // 32 row groups
+    const int64_t ps_stride = static_cast<int64_t>(kGnS + W) * kGnS;
     if (LDS_X) {
         for (int i = tid; i < nv; i += kGnBlock) x[i] = gx[i];
         __syncthreads();
     }
-    // forward: y[r] = (b[r] - sum_{c < r} L[r][c] y[c]) / L[r][r]
-    for (int k0 = 0; k0 < nv; k0 += kGnS) {
+    const int nsteps = (nv + kGnS - 1) / kGnS;
+    for (int step = nsteps - 1; step >= 0; --step) {
+        const int k0 = step * kGnS;
         const int sb = min(kGnS, nv - k0);
-        for (int t = wave; t < sb; t += WAVES) {   // off-block part: columns [r - W, k0)
-            const int r = k0 + t;
-            const double* Lr = Lb + static_cast<int64_t>(r) * ld;
-            double acc = 0.0;
-            for (int c = max(0, r - W) + lane; c < k0; c += 64) acc = fma(Lr[r - c], x[c], acc);
-            acc = wave_sum(acc);
-            if (lane == 0) x[r] -= acc;
+        const int n = min(nv, k0 + sb + W) - (k0 + sb);
+        const double* ps = PS + step * ps_stride;
+        // wave 0: column `lane` of the diagonal factor, loaded before the reduction
+        double lc[kGnS];
+        if (tid < 64) {
+#pragma unroll
+            for (int q = 0; q < kGnS; ++q) lc[q] = (lane < sb && q < sb) ? ps[q * kGnS + lane] : 0.0;
         }
-        for (int idx = tid; idx < sb * sb; idx += kGnBlock) {
-            const int t = idx / sb, q = idx % sb;
-            blk[t][q] = q <= t ? Lb[static_cast<int64_t>(k0 + t) * ld + (t - q)] : 0.0;
-        }
+        // v[t] = sum_r L[k0+sb+r][k0+t] x[k0+sb+r]
+        double acc = 0.0;
+        for (int r = g; r < n; r += G) acc = fma(ps[(kGnS + r) * kGnS + t], x[k0 + sb + r], acc);
+        acc += __shfl_xor(acc, 16, 64);
+        acc += __shfl_xor(acc, 32, 64);
+        if (lane < kGnS) part[wave][lane] = acc;
         __syncthreads();
-        if (tid < 64) {   // in-block lower-triangular solve, column oriented, one wave
-            double v = lane < sb ? x[k0 + lane] : 0.0;
-            for (int t = 0; t < sb; ++t) {
-                const double xt = __shfl(v, t, 64) / blk[t][t];
-                if (lane == t) v = xt;
-                if (lane > t && lane < sb) v -= blk[lane][t] * xt;
+        if (tid < 64) {
+            double v = 0.0;
+            if (lane < sb) {
+                double sum = 0.0;
+#pragma unroll
+                for (int w = 0; w < WAVES; ++w) sum += part[w][lane];
+                v = x[k0 + lane] - sum;
+            }
+            // L_D^T solve: x_t = (v_t - sum_{q>t} L[q][t] x_q) / L[t][t]
+#pragma unroll
+            for (int tt = kGnS - 1; tt >= 0; --tt) {
+                if (tt < sb) {
+                    const double xt = __shfl(v, tt, 64) / __shfl(lc[tt], tt, 64);
+                    if (lane == tt) v = xt;
+                    if (lane < tt) v -= lc[tt] * xt;
+                }
             }
             if (lane < sb) x[k0 + lane] = v;
-        }
-        __syncthreads();
-    }
-    // backward: dx[r] = (y[r] - sum_{c > r} L[c][r] dx[c]) / L[r][r]
-    for (int kend = nv; kend > 0; kend -= kGnS) {
-        const int k0 = max(0, kend - kGnS);
-        const int sb = kend - k0;
-        for (int idx = tid; idx < sb * sb; idx += kGnBlock) {
-            const int t = idx / sb, q = idx % sb;
-            blk[t][q] = q <= t ? Lb[static_cast<int64_t>(k0 + t) * ld + (t - q)] : 0.0;
-        }
-        __syncthreads();
-        if (tid < 64) {   // in-block upper-triangular (L^T) solve, one wave
-            double v = lane < sb ? x[k0 + lane] : 0.0;
-            for (int t = sb - 1; t >= 0; --t) {
-                const double xt = __shfl(v, t, 64) / blk[t][t];
-                if (lane == t) v = xt;
-                if (lane < t) v -= blk[t][lane] * xt;
-            }
-            if (lane < sb) x[k0 + lane] = v;
-        }
-        __syncthreads();
-        // subtract this block's contribution from rows c in [k0 - W, k0): x[c] -= sum_t L[k0+t][c] x[k0+t]
-        for (int c = max(0, k0 - W - kGnS) + tid; c < k0; c += kGnBlock) {
-            double acc = 0.0;
-            for (int t = 0; t < sb; ++t) {
-                const int r = k0 + t;
-                if (r - c <= W) acc = fma(Lb[static_cast<int64_t>(r) * ld + (r - c)], x[r], acc);
-            }
-            x[c] -= acc;
         }
         __syncthreads();
     }
@@ -355,18 +498,39 @@ __global__ __launch_bounds__(256) void gn_chi2_kernel(const double* __restrict__
 
 using namespace slamhip;
 
+static unsigned long long* g_gn_stamps = nullptr;
+
 extern "C" {
+
+// Diagnostics: device buffer of 5 uint64 receiving the factor kernel's
+// per-phase s_memtime totals (NULL disables).
+int slam_gn_set_stamps(void* dev_buf) {
+    g_gn_stamps = reinterpret_cast<unsigned long long*>(dev_buf);
+    return ok();
+}
+
+static int64_t window_dim(int32_t W) {
+    int64_t MP = 32;
+    while (MP < W + kGnS) MP <<= 1;
+    return MP;
+}
 
 int64_t slam_gn_work_size(int32_t N, int32_t E, int32_t W) {
     const int64_t nv = 3 * static_cast<int64_t>(N);
-    const int64_t M = W + kGnS;
-    return static_cast<int64_t>(E) * kGnContrib + nv * (W + 1) + nv + M * M + 8;
+    const int64_t MP = window_dim(W);
+    const int64_t steps = (nv + kGnS - 1) / kGnS;
+    return static_cast<int64_t>(E) * kGnContrib + nv * (W + 1) + nv + MP * (MP + 1) +
+           static_cast<int64_t>(kGnS) * lpw(W) + MP + steps * (kGnS + W) * kGnS + 8;
 }
 
 int slam_gn_max_lds_band(void) {
-    // largest W whose (W + S)^2 window fits the 160 KiB LDS
-    int W = 0;
-    while ((W + 1 + kGnS) * (W + 1 + kGnS) * 8 <= 160 * 1024) ++W;
+    // largest W whose power-of-two window + compact panel fit the LDS budget
+    int W = 2;
+    while (true) {
+        const int64_t MP = window_dim(W + 1);
+        if (sizeof(double) * (MP * (MP + 1) + static_cast<int64_t>(kGnS) * lpw(W + 1) + MP) + 4096 > 160 * 1024) break;
+        ++W;
+    }
     return W;
 }
 
@@ -392,22 +556,26 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
     if (n_slots > 0)
         hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128), dim3(128), 0, s, contrib, slot_rc,
                            slot_ptr, slot_items, n_slots, W, Hb, rhs);
-    const int M = W + kGnS;
-    const size_t win_bytes = sizeof(double) * static_cast<size_t>(M) * M;
-    if (W <= slam_gn_max_lds_band()) {
+    int MP = 32;
+    while (MP < W + kGnS) MP <<= 1;
+    const size_t lds_need = sizeof(double) * (static_cast<size_t>(MP) * (MP + 1) + static_cast<size_t>(kGnS) * lpw(W) + MP);
+    double* PS = gwin + static_cast<int64_t>(MP) * (MP + 1) + static_cast<int64_t>(kGnS) * lpw(W) + MP;
+    if (lds_need + 4096 <= 160 * 1024) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_factor_kernel<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(win_bytes));
-        hipLaunchKernelGGL(gn_factor_kernel<true>, dim3(1), dim3(kGnBlock), win_bytes, s, Hb, nv, W, gwin, status);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_need));
+        hipLaunchKernelGGL(gn_factor_kernel<true>, dim3(1), dim3(kGnFBlock), lds_need, s, Hb, rhs, nv, W, MP, gwin,
+                           gwin, PS, status, g_gn_stamps);
     } else {
-        hipLaunchKernelGGL(gn_factor_kernel<false>, dim3(1), dim3(kGnBlock), 0, s, Hb, nv, W, gwin, status);
+        hipLaunchKernelGGL(gn_factor_kernel<false>, dim3(1), dim3(kGnFBlock), 0, s, Hb, rhs, nv, W, MP, gwin,
+                           gwin + static_cast<int64_t>(MP) * (MP + 1), PS, status, g_gn_stamps);
     }
     const size_t x_bytes = sizeof(double) * static_cast<size_t>(nv);
     if (x_bytes <= 150 * 1024) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_solve_kernel<true>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_backsolve_kernel<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(x_bytes));
-        hipLaunchKernelGGL(gn_solve_kernel<true>, dim3(1), dim3(kGnBlock), x_bytes, s, Hb, nv, W, rhs);
+        hipLaunchKernelGGL(gn_backsolve_kernel<true>, dim3(1), dim3(kGnBlock), x_bytes, s, PS, nv, W, rhs);
     } else {
-        hipLaunchKernelGGL(gn_solve_kernel<false>, dim3(1), dim3(kGnBlock), 0, s, Hb, nv, W, rhs);
+        hipLaunchKernelGGL(gn_backsolve_kernel<false>, dim3(1), dim3(kGnBlock), 0, s, PS, nv, W, rhs);
     }
     hipLaunchKernelGGL(gn_update_kernel, dim3((N + 255) / 256), dim3(256), 0, s, poses, N, node_col, rhs);
     return check_launch("gn kernels");

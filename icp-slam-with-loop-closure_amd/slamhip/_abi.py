@@ -37,6 +37,7 @@ SIGNATURES = {
     "slam_pgo_orient_from_tf_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr]),
     "slam_gn_work_size": (c_i64, [c_int, c_int, c_int]),
     "slam_gn_max_lds_band": (c_int, []),
+    "slam_gn_set_stamps": (c_int, [c_ptr]),
     "slam_gn_iteration_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                       c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr]),
 }

@@ -160,6 +160,7 @@ int slam_icp_instance_shape(int i, int* block, int* qpt);
 int slam_icp_force_instance(int i);
 int slam_icp_selected_instance(int max_n1);
 int slam_icp_set_screen(int enable);
+int slam_gn_set_stamps(void* dev_buf);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=64, help="pairs in the CPU baseline sample")
     p.add_argument("--cpu-workers", type=int, default=16)
     p.add_argument("--instance", type=int, default=-1, help="force a kernel instance (diagnostics)")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
     return p.parse_args()
 
 
@@ -65,8 +66,13 @@ def init_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # SLAMHIP_ONE_DEVICE=1: every rank on cuda:0 (multi-rank dry run on a 1-GPU box, gloo)
+        dev = 0 if os.environ.get("SLAMHIP_ONE_DEVICE") == "1" else local
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -187,12 +193,20 @@ def main():
         # SE(2) edges + error + iteration count of every pair, padded to Bpad rows
         sd.pack(batch.out_tf[:B], batch.out_err[:B], batch.out_iters[:B], Bpad, out=buf)
 
+    def exchange():
+        if args.dist_backend == "nccl":
+            dist.all_gather_into_tensor(gathered, local_res)
+        else:   # gloo dry run: host staging
+            parts = [torch.empty_like(local_res, device="cpu") for _ in range(world)]
+            dist.all_gather(parts, local_res.cpu())
+            gathered.copy_(torch.stack(parts))
+
     def step():
         batch.launch()
         if world > 1:
             # SE(2) edges + error + iteration count of every pair -> every rank
             pack_results(local_res)
-            dist.all_gather_into_tensor(gathered, local_res)
+            exchange()
 
     for _ in range(args.warmup):
         step()
@@ -208,7 +222,7 @@ def main():
         ev[i][1].record(stream)
         if world > 1:
             pack_results(local_res)
-            dist.all_gather_into_tensor(gathered, local_res)
+            exchange()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -220,7 +234,8 @@ def main():
     n1 = ss.lens[1:B + 1]
     n2 = ss.lens[0:B]
     evals = float(np.sum(res.iters * n1 * n2))
-    t = torch.tensor([dt, evals, float(B), float(res.iters.sum())], dtype=torch.float64, device=ss.device)
+    t = torch.tensor([dt, evals, float(B), float(res.iters.sum())], dtype=torch.float64,
+                     device=ss.device if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
@@ -245,7 +260,9 @@ def main():
     tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
-            traffic = json.load(open(tpath)).get("icp_batch_bytes_per_launch")
+            tj = json.load(open(tpath))
+            # measured on tj["pairs"] pairs of this workload; scale to this launch
+            traffic = round(tj["icp_batch_bytes_per_launch"] * B / tj.get("pairs", B))
         except Exception:
             traffic = None
     sel = lib.slam_icp_selected_instance(int(n1.max()))

@@ -36,7 +36,7 @@ def main(tag):
     write = vals["WRITE_SIZE"] * 1024
     out = {"icp_batch_bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch, "write_bytes": write,
            "raw_FETCH_SIZE_KiB": vals["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": vals["WRITE_SIZE"],
-           "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one launch",
+           "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one launch", "pairs": 10000,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
            "tag": tag}
     json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)

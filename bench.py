@@ -174,7 +174,7 @@ def main():
     lib = _abi.lib()
     if args.instance >= 0:
         lib.slam_icp_force_instance(args.instance)
-    lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "1")))
+    lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)
     gathered = None

@@ -55,6 +55,8 @@ struct IcpArgs {
     // single-step mode
     int64_t* out_corr;
     const int64_t* corr_off;
+    // diagnostics: per-phase s_memtime totals of workgroup 0 (NULL = off)
+    unsigned long long* stamps;
 };
 
 // Squared distance with NumPy's rounding: sum((pc2[j] - q)**2) over x, y (+0).
@@ -123,6 +125,186 @@ __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf
     }
 }
 
+// Exact pruning of the chunked screen (PRUNE): one query per lane, chunks
+// visited outward from c0 (the chunk of the previous iteration's match of the
+// group's middle query), and a chunk is skipped when, for EVERY lane of the
+// wave, a conservative lower bound of its fp32 distances to the chunk's
+// bounding box exceeds the lane's current second-smallest chunk minimum M2.
+// Such a chunk cannot change (M1, M2) — both only ever decrease — nor C1
+// (strict < M1), so the result equals the full scan's.
+// Wave-wide min / max without LDS: DPP butterflies inside each 16-lane row,
+// then the four row results through SGPRs (v_readlane).
+#define SLAM_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+__device__ __forceinline__ float wave_min_f(float v) {
+    v = fminf(v, SLAM_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
+    v = fminf(v, SLAM_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
+    v = fminf(v, SLAM_DPP(v, 0x124));   // row_ror:4
+    v = fminf(v, SLAM_DPP(v, 0x128));   // row_ror:8
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fminf(fminf(r0, r1), fminf(r2, r3));
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+    v = fmaxf(v, SLAM_DPP(v, 0xB1));
+    v = fmaxf(v, SLAM_DPP(v, 0x4E));
+    v = fmaxf(v, SLAM_DPP(v, 0x124));
+    v = fmaxf(v, SLAM_DPP(v, 0x128));
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+#undef SLAM_DPP
+
+// Chunk-minimum update of (M1, M2, C1) with the minimum cm of chunk c.
+__device__ __forceinline__ void take_chunk(float cm, int c, float& M1, float& M2, int& C1) {
+    const bool lt = cm < M1;
+    M2 = __builtin_amdgcn_fmed3f(M1, M2, cm);
+    C1 = lt ? c * kChunk : C1;
+    M1 = fminf(M1, cm);
+}
+
+// Full scan of chunk c for one query per lane.
+__device__ __forceinline__ void scan_chunk(const float2* __restrict__ candf, int c, float qx, float qy,
+                                           float& M1, float& M2, int& C1) {
+    const int j0 = c * kChunk;
+    float ca = INFINITY, cb = INFINITY;   // two partial minima: half the dependency chain
+#pragma unroll 4
+    for (int j = j0; j < j0 + kChunk; j += 4) {
+        const float4 p0 = *reinterpret_cast<const float4*>(candf + j);
+        const float4 p1 = *reinterpret_cast<const float4*>(candf + j + 2);
+        ca = fminf(ca, fminf(screen_d32(p0.x, p0.y, qx, qy), screen_d32(p0.z, p0.w, qx, qy)));
+        cb = fminf(cb, fminf(screen_d32(p1.x, p1.y, qx, qy), screen_d32(p1.z, p1.w, qx, qy)));
+    }
+    take_chunk(fminf(ca, cb), c, M1, M2, C1);
+}
+
+// Conservative squared distance between two axis-aligned boxes (or a point,
+// as a degenerate box), rounded DOWN by 1e-6 relative: a lower bound of every
+// fp32 screened distance between their points (>> the ~16 u of rounding).
+__device__ __forceinline__ float box_lb(float ax0, float ax1, float ay0, float ay1, const float4& b) {
+    const float ddx = fmaxf(fmaxf(b.x - ax1, ax0 - b.y), 0.0f);
+    const float ddy = fmaxf(fmaxf(b.z - ay1, ay0 - b.w), 0.0f);
+    return fmaf(ddy, ddy, ddx * ddx) * (1.0f - 1e-6f);
+}
+
+// 128-bit chunk masks (two words): next live chunk >= p / <= p, or nch / -1.
+__device__ __forceinline__ int mask_up(uint64_t lo, uint64_t hi, int p, int nch) {
+    if (p < 64) {
+        const uint64_t m = lo & (~0ull << p);
+        if (m) return __builtin_ctzll(m);
+        p = 64;
+    }
+    if (p < 128) {
+        const uint64_t m = hi & (~0ull << (p - 64));
+        if (m) return 64 + __builtin_ctzll(m);
+    }
+    return nch;
+}
+__device__ __forceinline__ int mask_down(uint64_t lo, uint64_t hi, int p) {
+    if (p >= 64) {
+        const int q = p - 64;
+        const uint64_t m = q == 63 ? hi : (hi & ((2ull << q) - 1));
+        if (m) return 64 + 63 - __builtin_clzll(m);
+        p = 63;
+    }
+    if (p >= 0) {
+        const uint64_t m = p == 63 ? lo : (lo & ((2ull << p) - 1));
+        if (m) return 63 - __builtin_clzll(m);
+    }
+    return -1;
+}
+
+// Exact pruning of the chunked screen (PRUNE).  Lane l of wave w holds query
+// k * BLOCK + 64 w + l for every k: each (wave, k) "group" is 64 consecutive
+// scan points.  Per group:
+//   1. seed: scan chunk c0_k (the previous iteration's match of the group's
+//      middle query, or the proportional index) and its two neighbours — the
+//      QPT groups interleaved for ILP -> per-lane (M1, M2, C1);
+//   2. vector test: lane l tests chunks l and l+64 against the group's query
+//      bounding box and the group's largest M2 -> 128-bit mask of chunks that
+//      may still hold a value below some lane's M2;
+//   3. visit those chunks nearest-first; each is skipped when EVERY lane's own
+//      lower bound exceeds its current M2.
+// A skipped chunk cannot change (M1, M2) — both only decrease — nor C1 (strict
+// < M1), so (M1, M2, C1) equal the full scan's.
+template <int QPT>
+__device__ __forceinline__ void nn_scan_pruned(const float2* __restrict__ candf, const float4* __restrict__ box,
+                                               int nch, const float (&qx)[QPT], const float (&qy)[QPT],
+                                               const bool (&valid)[QPT], const int (&c0)[QPT], float (&M1)[QPT],
+                                               float (&M2)[QPT], int (&C1)[QPT], int& nscanned) {
+    const int lane = threadIdx.x & 63;
+    int s0[QPT], s1[QPT];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+        s0[k] = max(0, min(c0[k] - 1, nch - 3));
+        s1[k] = min(nch, s0[k] + 3);
+    }
+    // 1. seed chunks, the QPT groups interleaved
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        float cm[QPT];
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) cm[k] = INFINITY;
+#pragma unroll 2
+        for (int t = 0; t < kChunk; t += 2) {
+#pragma unroll
+            for (int k = 0; k < QPT; ++k) {
+                if (s0[k] + q < s1[k]) {
+                    const float4 pp = *reinterpret_cast<const float4*>(candf + (s0[k] + q) * kChunk + t);
+                    cm[k] = fminf(cm[k], fminf(screen_d32(pp.x, pp.y, qx[k], qy[k]),
+                                               screen_d32(pp.z, pp.w, qx[k], qy[k])));
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            if (s0[k] + q < s1[k]) {
+                take_chunk(cm[k], s0[k] + q, M1[k], M2[k], C1[k]);
+                ++nscanned;
+            }
+        }
+    }
+    // 2. group boxes and masks
+    uint64_t mlo[QPT], mhi[QPT];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+        const float gx0 = wave_min_f(valid[k] ? qx[k] : INFINITY);
+        const float gx1 = wave_max_f(valid[k] ? qx[k] : -INFINITY);
+        const float gy0 = wave_min_f(valid[k] ? qy[k] : INFINITY);
+        const float gy1 = wave_max_f(valid[k] ? qy[k] : -INFINITY);
+        const float gM2 = wave_max_f(valid[k] ? M2[k] : -INFINITY);
+        const int cl = lane, ch = 64 + lane;
+        const bool nl = cl < nch && (cl < s0[k] || cl >= s1[k]) && box_lb(gx0, gx1, gy0, gy1, box[cl]) <= gM2;
+        const bool nh = ch < nch && (ch < s0[k] || ch >= s1[k]) && box_lb(gx0, gx1, gy0, gy1, box[ch]) <= gM2;
+        mlo[k] = __ballot(nl);
+        mhi[k] = __ballot(nh);
+    }
+    // 3. live chunks, nearest to the seed first
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+        int up = mask_up(mlo[k], mhi[k], s1[k], nch);
+        int dn = mask_down(mlo[k], mhi[k], s0[k] - 1);
+        while (up < nch || dn >= 0) {
+            int c;
+            if (up < nch && (dn < 0 || up - s1[k] <= s0[k] - 1 - dn)) {
+                c = up;
+                up = mask_up(mlo[k], mhi[k], up + 1, nch);
+            } else {
+                c = dn;
+                dn = mask_down(mlo[k], mhi[k], dn - 1);
+            }
+            const float lb = box_lb(qx[k], qx[k], qy[k], qy[k], box[c]);
+            if (__all(!valid[k] || lb > M2[k])) continue;
+            scan_chunk(candf, c, qx[k], qy[k], M1[k], M2[k], C1[k]);
+            ++nscanned;
+        }
+    }
+}
+
 // Lower bound of the exact squared distance T of any candidate whose fp32
 // screened distance is >= d32 (DESIGN.md §"fp32 screen, exact answer"):
 // d32 <= F(T) = (1+8u) T + 3a sqrt(T) + 3a^2 with u = 2^-24 and a the
@@ -138,7 +320,7 @@ __device__ __forceinline__ double screen_lower_bound(double d32, double a) {
     return s * s * (1.0 - 1e-12);
 }
 
-template <int BLOCK, int QPT, bool STEP, bool SCREEN>
+template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false>
 __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -150,6 +332,7 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     float2* candf = reinterpret_cast<float2*>(cand + cap);
     int* fq = reinterpret_cast<int*>(candf + cap);          // [WAVES][64*QPT] query ids
     int* fres = fq + WAVES * 64 * QPT;                       // [WAVES][64*QPT] exact answers
+    float4* box = reinterpret_cast<float4*>(fres + WAVES * 64 * QPT);   // PRUNE: [cap/32] chunk boxes
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -180,6 +363,25 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                 candf[j] = make_float2(kSentinel, kSentinel);
         }
     }
+    const int nch = (n2 + kChunk - 1) / kChunk;
+    if constexpr (SCREEN && PRUNE) {
+        __syncthreads();   // candf complete
+        for (int c = tid; c < nch; c += BLOCK) {
+            float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+            for (int j = c * kChunk; j < min(n2, (c + 1) * kChunk); ++j) {
+                const float2 p = candf[j];
+                x0 = fminf(x0, p.x);
+                x1 = fmaxf(x1, p.x);
+                y0 = fminf(y0, p.y);
+                y1 = fmaxf(y1, p.y);
+            }
+            box[c] = make_float4(x0, x1, y0, y1);
+        }
+    }
+    int bprev[QPT];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) bprev[k] = -1;
+    int nscan_total = 0;
     bool screen = false;
     if constexpr (SCREEN) {
         double cm[1] = {cmax};
@@ -207,6 +409,24 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     __syncthreads();
 
     double last_err = 0.0;
+    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0;
+
+    const bool stamping = a.stamps != nullptr && b == 0 && tid == 0;
+    auto stamp = [&](int ph) {
+        if (stamping) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (ph >= 0) tph[ph] += t - tprev;
+            tprev = t;
+        }
+    };
+    auto flush_stamps = [&]() {
+        if (stamping) {
+            for (int q = 0; q < 4; ++q) a.stamps[q] = tph[q];
+            a.stamps[4] = static_cast<unsigned long long>(nscan_total);   // chunks scanned (wave 0)
+
+        }
+    };
+    stamp(-1);
     for (int it = 0;; ++it) {
         double qx[QPT], qy[QPT];
         int bi[QPT];
@@ -232,7 +452,25 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                     M2[k] = INFINITY;
                     C1[k] = 0;
                 }
-                if (screen) nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
+                if (screen) {
+                    if constexpr (PRUNE) {
+                        int c0[QPT];
+                        bool vq[QPT];
+#pragma unroll
+                        for (int k = 0; k < QPT; ++k) {
+                            const int mid = __builtin_amdgcn_readfirstlane(k * BLOCK + wave * 64 + 32);
+                            const int prev = __builtin_amdgcn_readlane(bprev[k], 32);
+                            c0[k] = prev >= 0 ? prev / kChunk
+                                              : static_cast<int>(static_cast<int64_t>(mid) * n2 / max(n1, 1)) / kChunk;
+                            c0[k] = min(max(c0[k], 0), nch - 1);
+                            vq[k] = k * BLOCK + tid < n1;
+                        }
+                        nn_scan_pruned<QPT>(candf, box, nch, fx, fy, vq, c0, M1, M2, C1, nscan_total);
+                    } else {
+                        nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
+                    }
+                }
+                stamp(0);
                 // ---- certify: the screened winner is the exact fp64 argmin? ---
                 int base = 0;
 #pragma unroll
@@ -280,6 +518,7 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                     }
                     base += __popcll(fails);
                 }
+                stamp(1);
                 // ---- wave-cooperative exact fallback for uncertified queries ---
                 for (int t = 0; t < base; ++t) {
                     const int i = fq[wave * 64 * QPT + t];
@@ -309,9 +548,12 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                 }
             }
             __syncthreads();   // fres visible to every lane of the wave
+            stamp(2);
 #pragma unroll
-            for (int k = 0; k < QPT; ++k)
+            for (int k = 0; k < QPT; ++k) {
                 if (bi[k] < 0) bi[k] = fres[wave * 64 * QPT + (-1 - bi[k])];
+                bprev[k] = k * BLOCK + tid < n1 ? bi[k] : -1;
+            }
         } else {
             // ---- exact fp64 scan (src/icp.py:62-63) ---------------------------
             double best[QPT];
@@ -402,6 +644,7 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
         D.m10 = si; D.m11 = c;   D.m12 = ty;
         const SE2 Tn = se2_mul(D, T);   // src/icp.py:67
 
+        stamp(3);
         if constexpr (STEP) {
             if (tid == 0) {
                 store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
@@ -422,6 +665,7 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
             last_err = err;
             T = Tn;
             if (stop) {
+                flush_stamps();
                 if (tid == 0) {
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
@@ -445,13 +689,16 @@ struct Instance {
     int qpt;
     KernelFn batch;          // exact fp64 scan
     KernelFn step;
-    KernelFn batch_screen;   // fp32 screen + exact certification
+    KernelFn batch_screen;   // fp32 screen + exact certification, every chunk
     KernelFn step_screen;
+    KernelFn batch_prune;    // fp32 screen with exact chunk pruning (default)
+    KernelFn step_prune;
 };
 
 #define SLAM_INST(B, Q)                                                                   \
     {B, Q, icp_kernel<B, Q, false, false>, icp_kernel<B, Q, true, false>,                 \
-     icp_kernel<B, Q, false, true>, icp_kernel<B, Q, true, true>}
+     icp_kernel<B, Q, false, true>, icp_kernel<B, Q, true, true>,                         \
+     icp_kernel<B, Q, false, true, true>, icp_kernel<B, Q, true, true, true>}
 static const Instance kInstances[] = {
     SLAM_INST(64, 1),   SLAM_INST(64, 2),   SLAM_INST(64, 4),   SLAM_INST(128, 3),
     SLAM_INST(128, 4),  SLAM_INST(192, 4),  SLAM_INST(192, 6),  SLAM_INST(256, 4),
@@ -538,20 +785,28 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
     }
 }
 
-static int g_screen = 1;
+// NN search mode: 0 exact fp64 scan, 1 fp32 screen (all chunks), 2 fp32
+// screen with exact chunk pruning (default).  Results are identical in all
+// three (tests/test_icp_gpu.py::test_nn_modes_identical).
+static int g_screen = 2;
+static unsigned long long* g_icp_stamps = nullptr;
 
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
                   void* stream) {
     const Instance* inst = pick_instance(max_n1, g_forced_instance);
     if (!inst) return fail(SLAM_ETOOBIG, "query scan of %d points exceeds capacity %d", max_n1, kMaxQuery);
     IcpArgs a = args;
+    a.stamps = g_icp_stamps;
     a.cand_cap = max_n2 < kCandCap ? ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk : kCandCap;
-    const bool screen = g_screen && max_n2 <= kCandCap;
+    const int mode = max_n2 <= kCandCap ? g_screen : 0;
     size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
-    if (screen)
+    if (mode >= 1)
         lds += static_cast<size_t>(a.cand_cap) * sizeof(float2) +
                2 * sizeof(int) * static_cast<size_t>(inst->block) * inst->qpt;
-    KernelFn fn = screen ? (step ? inst->step_screen : inst->batch_screen) : (step ? inst->step : inst->batch);
+    if (mode == 2) lds += static_cast<size_t>(a.cand_cap / kChunk) * sizeof(float4);
+    KernelFn fn = mode == 2 ? (step ? inst->step_prune : inst->batch_prune)
+                : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)
+                            : (step ? inst->step : inst->batch);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds));
     hipLaunchKernelGGL(fn, dim3(B), dim3(inst->block), lds, as_stream(stream), a);
@@ -583,8 +838,13 @@ int slam_icp_force_instance(int i) {
     g_forced_instance = (i >= 0 && i < kNumInstances) ? i : -1;
     return ok();
 }
-int slam_icp_set_screen(int enable) {
-    g_screen = enable ? 1 : 0;
+int slam_icp_set_stamps(void* dev_buf) {
+    g_icp_stamps = reinterpret_cast<unsigned long long*>(dev_buf);
+    return ok();
+}
+int slam_icp_set_screen(int mode) {
+    if (mode < 0 || mode > 2) return fail(SLAM_EINVAL, "nn mode %d not in {0, 1, 2}", mode);
+    g_screen = mode;
     return ok();
 }
 int slam_icp_selected_instance(int max_n1) {

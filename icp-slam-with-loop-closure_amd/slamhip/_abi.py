@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libslamhip.so")
+# SLAMHIP_LIB overrides the library path (A/B builds in diagnostics only)
+LIB_PATH = os.environ.get("SLAMHIP_LIB") or os.path.join(_HERE, "libslamhip.so")
 
 c_int = ctypes.c_int32
 c_i64 = ctypes.c_int64
@@ -26,6 +27,7 @@ SIGNATURES = {
     "slam_icp_force_instance": (c_int, [c_int]),
     "slam_icp_selected_instance": (c_int, [c_int]),
     "slam_icp_set_screen": (c_int, [c_int]),
+    "slam_icp_set_stamps": (c_int, [c_ptr]),
     "slam_icp_batch_f64": (c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_dbl, c_int, c_dbl, c_int,
                                    c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "slam_icp_step_f64": (c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_int, c_int, c_int,

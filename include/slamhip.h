@@ -159,8 +159,11 @@ int slam_icp_num_instances(void);
 int slam_icp_instance_shape(int i, int* block, int* qpt);
 int slam_icp_force_instance(int i);
 int slam_icp_selected_instance(int max_n1);
-int slam_icp_set_screen(int enable);
+/* NN search mode: 0 exact fp64 scan, 1 fp32 screen (all chunks), 2 fp32
+ * screen with exact chunk pruning (default); identical results. */
+int slam_icp_set_screen(int mode);
 int slam_gn_set_stamps(void* dev_buf);
+int slam_icp_set_stamps(void* dev_buf);
 
 #ifdef __cplusplus
 }

@@ -175,3 +175,28 @@ def test_bad_inputs_raise(icp):
         icp.get_correspondences(pc, pc)
     with pytest.raises(ValueError):
         icp.icp(np.zeros((0, 3)), np.ones((3, 3)))
+
+
+def test_nn_modes_identical(k):
+    """Exact fp64 scan, fp32 screen and pruned fp32 screen: bit-identical
+    correspondences, hence bit-identical transforms, errors and iterations."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 24
+    seq, inits = _sequence_pairs(n, seed=9)
+    outs = []
+    try:
+        for mode in (0, 1, 2):
+            assert lib.slam_icp_set_screen(mode) == 0
+            outs.append(k.icp_batch(seq.scans, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05,
+                                    max_iters=100, history=True))
+            _, corr, _ = k.icp_step(seq.scans, np.arange(1, n + 1), np.arange(0, n), inits)
+            outs[-1].corr = np.concatenate(corr)
+    finally:
+        lib.slam_icp_set_screen(2)
+    for o in outs[1:]:
+        assert np.array_equal(o.corr, outs[0].corr)
+        assert np.array_equal(o.iters, outs[0].iters)
+        assert np.array_equal(o.tf, outs[0].tf) and np.array_equal(o.err, outs[0].err)
+        for h0, h1 in zip(outs[0].hist, o.hist):
+            assert np.array_equal(h0, h1)

@@ -16,7 +16,7 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 inst = int(os.environ.get("SLAMHIP_INSTANCE", "-1"))
 lib = _abi.lib()
 lib.slam_icp_force_instance(inst)
-lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "1")))
+lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
 seq = synthetic.make_sequence(pairs + 1, seed=2025)
 inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, pairs + 1)])
 ss = k.ScanSet(seq.scans)

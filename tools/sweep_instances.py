@@ -23,16 +23,19 @@ def main():
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, pairs + 1)])
     ss = k.ScanSet(seq.scans)
     lib = _abi.lib()
-    lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "1")))
+    lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     b, q = ctypes.c_int32(), ctypes.c_int32()
     rows = []
-    for i in [-1] + list(range(lib.slam_icp_num_instances())):
+    only = os.environ.get("SWEEP_INSTANCES")
+    cand = [int(x) for x in only.split(",")] if only else [-1] + list(range(lib.slam_icp_num_instances()))
+    sizes = (pairs,) if only else (pairs // 4, pairs // 2, pairs)
+    for i in cand:
         if i >= 0:
             lib.slam_icp_instance_shape(i, ctypes.byref(b), ctypes.byref(q))
             if b.value * q.value < ss.lens.max():
                 continue
         lib.slam_icp_force_instance(i)
-        for B in (pairs // 4, pairs // 2, pairs):
+        for B in sizes:
             batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits[:B], epsilon=0.05, max_iters=100)
             batch.launch()
             torch.cuda.synchronize()

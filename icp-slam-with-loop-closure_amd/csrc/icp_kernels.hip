@@ -59,6 +59,14 @@ struct IcpArgs {
     unsigned long long* stamps;
 };
 
+// A wave-uniform double moved to SGPRs (v_readfirstlane of both halves).
+__device__ __forceinline__ double uniform_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane(static_cast<int>(b & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane(static_cast<int>(b >> 32));
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
 // Squared distance with NumPy's rounding: sum((pc2[j] - q)**2) over x, y (+0).
 __device__ __forceinline__ double exact_d2(double px, double py, double qx, double qy) {
     const double dx = px - qx;
@@ -157,6 +165,16 @@ __device__ __forceinline__ float wave_max_f(float v) {
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
     return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+    v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
+    v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x124, 0xF, 0xF, false));
+    v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x128, 0xF, 0xF, false));
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0) |
+                                 __builtin_amdgcn_readlane(static_cast<int>(v), 16) |
+                                 __builtin_amdgcn_readlane(static_cast<int>(v), 32) |
+                                 __builtin_amdgcn_readlane(static_cast<int>(v), 48));
+}
 #undef SLAM_DPP
 
 // Chunk-minimum update of (M1, M2, C1) with the minimum cm of chunk c.
@@ -191,118 +209,120 @@ __device__ __forceinline__ float box_lb(float ax0, float ax1, float ay0, float a
     return fmaf(ddy, ddy, ddx * ddx) * (1.0f - 1e-6f);
 }
 
-// 128-bit chunk masks (two words): next live chunk >= p / <= p, or nch / -1.
-__device__ __forceinline__ int mask_up(uint64_t lo, uint64_t hi, int p, int nch) {
-    if (p < 64) {
-        const uint64_t m = lo & (~0ull << p);
-        if (m) return __builtin_ctzll(m);
-        p = 64;
-    }
-    if (p < 128) {
-        const uint64_t m = hi & (~0ull << (p - 64));
-        if (m) return 64 + __builtin_ctzll(m);
-    }
-    return nch;
-}
-__device__ __forceinline__ int mask_down(uint64_t lo, uint64_t hi, int p) {
-    if (p >= 64) {
-        const int q = p - 64;
-        const uint64_t m = q == 63 ? hi : (hi & ((2ull << q) - 1));
-        if (m) return 64 + 63 - __builtin_clzll(m);
-        p = 63;
-    }
-    if (p >= 0) {
-        const uint64_t m = p == 63 ? lo : (lo & ((2ull << p) - 1));
-        if (m) return 63 - __builtin_clzll(m);
-    }
-    return -1;
+// Exact pruned screen (PRUNE).  Each lane tracks, for its query, the smallest
+// fp32 screened distance M1 with its FIRST index J1 and the second smallest M2
+// over all other candidates — exactly what the full screen yields — while
+// skipping candidates that provably cannot change them:
+//   1. window: the kWin sub-chunks (of kSub candidates) around the lane's
+//      predicted match p (last iteration's match) are scanned in full, the QPT
+//      queries interleaved for ILP;
+//   2. group mask: lane l of the wave tests chunks l and l+64 (of kChunk) with
+//      the bounding box of the wave's 64 queries against the wave's largest M2
+//      -> 128-bit mask of chunks that may hold anything below some lane's M2;
+//   3. visits: every sub-chunk of a live chunk that lies outside the lane's
+//      window and whose box is within the lane's current M2 is scanned.
+// Skipped candidates have d32 >= lower bound > M2 at the time of the test, and
+// M2 only decreases, so (M1, M2, J1) equal the full scan's.
+constexpr int kSub = 8;
+constexpr int kWin = 3;
+constexpr int kBatch = 8;     // live sub-chunks tested per batch
+
+__device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, int& J1) {
+    const bool lt = d < M1;
+    M2 = __builtin_amdgcn_fmed3f(M1, M2, d);
+    J1 = lt ? j : J1;
+    M1 = fminf(M1, d);
 }
 
-// Exact pruning of the chunked screen (PRUNE).  Lane l of wave w holds query
-// k * BLOCK + 64 w + l for every k: each (wave, k) "group" is 64 consecutive
-// scan points.  Per group:
-//   1. seed: scan chunk c0_k (the previous iteration's match of the group's
-//      middle query, or the proportional index) and its two neighbours — the
-//      QPT groups interleaved for ILP -> per-lane (M1, M2, C1);
-//   2. vector test: lane l tests chunks l and l+64 against the group's query
-//      bounding box and the group's largest M2 -> 128-bit mask of chunks that
-//      may still hold a value below some lane's M2;
-//   3. visit those chunks nearest-first; each is skipped when EVERY lane's own
-//      lower bound exceeds its current M2.
-// A skipped chunk cannot change (M1, M2) — both only decrease — nor C1 (strict
-// < M1), so (M1, M2, C1) equal the full scan's.
 template <int QPT>
-__device__ __forceinline__ void nn_scan_pruned(const float2* __restrict__ candf, const float4* __restrict__ box,
-                                               int nch, const float (&qx)[QPT], const float (&qy)[QPT],
-                                               const bool (&valid)[QPT], const int (&c0)[QPT], float (&M1)[QPT],
-                                               float (&M2)[QPT], int (&C1)[QPT], int& nscanned) {
+__device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ candf,
+                                                 const float4* __restrict__ box8, int nsub,
+                                                 const float (&qx)[QPT], const float (&qy)[QPT],
+                                                 const bool (&valid)[QPT], const int (&pred)[QPT],
+                                                 float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
+                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[3]) {
     const int lane = threadIdx.x & 63;
-    int s0[QPT], s1[QPT];
+    unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
+    auto lap = [&](int q) {   // diagnostics: sub-phase s_memtime (workgroup 0, wave 0)
+        if (stamping) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            if (q == 0) tsub[0] += t1 - t0;
+            if (q == 1) tsub[1] += t1 - t0;
+            if (q == 2) tsub[2] += t1 - t0;
+            t0 = t1;
+        }
+    };
+    int ws[QPT];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) ws[k] = min(max((pred[k] >> 3) - 1, 0), nsub - kWin);
+    // 1. windows (J1 holds the offset inside the window until the end of the loop)
+#pragma unroll 2
+    for (int t = 0; t < kWin * kSub; t += 2) {
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const float4 pp = *reinterpret_cast<const float4*>(candf + ws[k] * kSub + t);
+            take_cand(screen_d32(pp.x, pp.y, qx[k], qy[k]), t, M1[k], M2[k], J1[k]);
+            take_cand(screen_d32(pp.z, pp.w, qx[k], qy[k]), t + 1, M1[k], M2[k], J1[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) J1[k] += ws[k] * kSub;
+    lap(0);
+    // 2. group boxes and largest M2, all groups interleaved
+    float gx0[QPT], gx1[QPT], gy0[QPT], gy1[QPT], gM2[QPT];
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-        s0[k] = max(0, min(c0[k] - 1, nch - 3));
-        s1[k] = min(nch, s0[k] + 3);
+        gx0[k] = wave_min_f(valid[k] ? qx[k] : INFINITY);
+        gx1[k] = wave_max_f(valid[k] ? qx[k] : -INFINITY);
+        gy0[k] = wave_min_f(valid[k] ? qy[k] : INFINITY);
+        gy1[k] = wave_max_f(valid[k] ? qy[k] : -INFINITY);
+        gM2[k] = wave_max_f(valid[k] ? M2[k] : -INFINITY);
     }
-    // 1. seed chunks, the QPT groups interleaved
+    lap(1);
+    // 3. per group, per 64-sub-chunk word: lane l tests sub-chunk 64 w + l
+    //    against the group box -> live mask; each live sub-chunk is tested by
+    //    every lane against its own query (batches of kBatch, independent loads),
+    //    the wave OR of those bits says which sub-chunks to scan.
+    const int nw = (nsub + 63) >> 6;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        float cm[QPT];
+    for (int k = 0; k < QPT; ++k) {
+        for (int w = 0; w < nw; ++w) {
+            const int sl = 64 * w + lane;
+            uint64_t live = __ballot(sl < nsub && box_lb(gx0[k], gx1[k], gy0[k], gy1[k], box8[sl]) <= gM2[k]);
+            while (live) {
+                // up to kBatch live sub-chunks per batch, straight-line: the box
+                // reads (broadcast) and tests issue back to back
+                int sc[kBatch];
+                uint32_t need = 0;
 #pragma unroll
-        for (int k = 0; k < QPT; ++k) cm[k] = INFINITY;
-#pragma unroll 2
-        for (int t = 0; t < kChunk; t += 2) {
+                for (int u = 0; u < kBatch; ++u) {
+                    const bool has = live != 0;
+                    sc[u] = has ? 64 * w + static_cast<int>(__builtin_ctzll(live | (1ull << 63))) : 0;
+                    live &= live - 1;
+                    const bool nd = has && valid[k] && (sc[u] < ws[k] || sc[u] >= ws[k] + kWin) &&
+                                    box_lb(qx[k], qx[k], qy[k], qy[k], box8[sc[u]]) <= M2[k];
+                    need |= static_cast<uint32_t>(nd) << u;
+                }
+                const uint32_t anyneed = wave_or_u32(need);
 #pragma unroll
-            for (int k = 0; k < QPT; ++k) {
-                if (s0[k] + q < s1[k]) {
-                    const float4 pp = *reinterpret_cast<const float4*>(candf + (s0[k] + q) * kChunk + t);
-                    cm[k] = fminf(cm[k], fminf(screen_d32(pp.x, pp.y, qx[k], qy[k]),
-                                               screen_d32(pp.z, pp.w, qx[k], qy[k])));
+                for (int u = 0; u < kBatch; ++u) {
+                    if ((anyneed >> u) & 1u) {
+                        ++nvisit;
+                        if ((need >> u) & 1u) {
+                            const int c8 = sc[u] * kSub;
+#pragma unroll
+                            for (int t = 0; t < kSub; t += 2) {
+                                const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
+                                take_cand(screen_d32(pp.x, pp.y, qx[k], qy[k]), c8 + t, M1[k], M2[k], J1[k]);
+                                take_cand(screen_d32(pp.z, pp.w, qx[k], qy[k]), c8 + t + 1, M1[k], M2[k], J1[k]);
+                            }
+                        }
+                    }
                 }
             }
         }
-#pragma unroll
-        for (int k = 0; k < QPT; ++k) {
-            if (s0[k] + q < s1[k]) {
-                take_chunk(cm[k], s0[k] + q, M1[k], M2[k], C1[k]);
-                ++nscanned;
-            }
-        }
     }
-    // 2. group boxes and masks
-    uint64_t mlo[QPT], mhi[QPT];
-#pragma unroll
-    for (int k = 0; k < QPT; ++k) {
-        const float gx0 = wave_min_f(valid[k] ? qx[k] : INFINITY);
-        const float gx1 = wave_max_f(valid[k] ? qx[k] : -INFINITY);
-        const float gy0 = wave_min_f(valid[k] ? qy[k] : INFINITY);
-        const float gy1 = wave_max_f(valid[k] ? qy[k] : -INFINITY);
-        const float gM2 = wave_max_f(valid[k] ? M2[k] : -INFINITY);
-        const int cl = lane, ch = 64 + lane;
-        const bool nl = cl < nch && (cl < s0[k] || cl >= s1[k]) && box_lb(gx0, gx1, gy0, gy1, box[cl]) <= gM2;
-        const bool nh = ch < nch && (ch < s0[k] || ch >= s1[k]) && box_lb(gx0, gx1, gy0, gy1, box[ch]) <= gM2;
-        mlo[k] = __ballot(nl);
-        mhi[k] = __ballot(nh);
-    }
-    // 3. live chunks, nearest to the seed first
-#pragma unroll
-    for (int k = 0; k < QPT; ++k) {
-        int up = mask_up(mlo[k], mhi[k], s1[k], nch);
-        int dn = mask_down(mlo[k], mhi[k], s0[k] - 1);
-        while (up < nch || dn >= 0) {
-            int c;
-            if (up < nch && (dn < 0 || up - s1[k] <= s0[k] - 1 - dn)) {
-                c = up;
-                up = mask_up(mlo[k], mhi[k], up + 1, nch);
-            } else {
-                c = dn;
-                dn = mask_down(mlo[k], mhi[k], dn - 1);
-            }
-            const float lb = box_lb(qx[k], qx[k], qy[k], qy[k], box[c]);
-            if (__all(!valid[k] || lb > M2[k])) continue;
-            scan_chunk(candf, c, qx[k], qy[k], M1[k], M2[k], C1[k]);
-            ++nscanned;
-        }
-    }
+    lap(2);
 }
 
 // Lower bound of the exact squared distance T of any candidate whose fp32
@@ -320,8 +340,8 @@ __device__ __forceinline__ double screen_lower_bound(double d32, double a) {
     return s * s * (1.0 - 1e-12);
 }
 
-template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false>
-__global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
+template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false, int WPE = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void icp_kernel(IcpArgs a) {
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* red0 = reinterpret_cast<double*>(smem);
@@ -332,7 +352,7 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     float2* candf = reinterpret_cast<float2*>(cand + cap);
     int* fq = reinterpret_cast<int*>(candf + cap);          // [WAVES][64*QPT] query ids
     int* fres = fq + WAVES * 64 * QPT;                       // [WAVES][64*QPT] exact answers
-    float4* box = reinterpret_cast<float4*>(fres + WAVES * 64 * QPT);   // PRUNE: [cap/32] chunk boxes
+    float4* box8 = reinterpret_cast<float4*>(fres + WAVES * 64 * QPT);   // PRUNE: [cap/8] sub-chunk boxes
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -363,19 +383,19 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                 candf[j] = make_float2(kSentinel, kSentinel);
         }
     }
-    const int nch = (n2 + kChunk - 1) / kChunk;
+    const int nsub = (n2 + kChunk - 1) / kChunk * (kChunk / kSub);   // sub-chunks incl. padding
     if constexpr (SCREEN && PRUNE) {
         __syncthreads();   // candf complete
-        for (int c = tid; c < nch; c += BLOCK) {
+        for (int c = tid; c < nsub; c += BLOCK) {
             float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
-            for (int j = c * kChunk; j < min(n2, (c + 1) * kChunk); ++j) {
+            for (int j = c * kSub; j < min(n2, (c + 1) * kSub); ++j) {
                 const float2 p = candf[j];
                 x0 = fminf(x0, p.x);
                 x1 = fmaxf(x1, p.x);
                 y0 = fminf(y0, p.y);
                 y1 = fmaxf(y1, p.y);
             }
-            box[c] = make_float4(x0, x1, y0, y1);
+            box8[c] = make_float4(x0, x1, y0, y1);
         }
     }
     int bprev[QPT];
@@ -409,9 +429,9 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
     __syncthreads();
 
     double last_err = 0.0;
-    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0;
+    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[3] = {0, 0, 0};
 
-    const bool stamping = a.stamps != nullptr && b == 0 && tid == 0;
+    const bool stamping = a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
     auto stamp = [&](int ph) {
         if (stamping) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -420,14 +440,15 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
         }
     };
     auto flush_stamps = [&]() {
-        if (stamping) {
+        if (stamping && lane == 0) {
             for (int q = 0; q < 4; ++q) a.stamps[q] = tph[q];
-            a.stamps[4] = static_cast<unsigned long long>(nscan_total);   // chunks scanned (wave 0)
-
+            a.stamps[4] = static_cast<unsigned long long>(nscan_total);   // sub-chunks visited (wave 0)
+            for (int q = 0; q < 3; ++q) a.stamps[5 + q] = tsub[q];
         }
     };
     stamp(-1);
     for (int it = 0;; ++it) {
+        asm volatile("" ::: "memory");   // keep pc1 re-loads inside the loop (registers, not LICM)
         double qx[QPT], qy[QPT];
         int bi[QPT];
         if constexpr (SCREEN) {
@@ -454,18 +475,17 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                 }
                 if (screen) {
                     if constexpr (PRUNE) {
-                        int c0[QPT];
+                        int pred[QPT];
                         bool vq[QPT];
 #pragma unroll
                         for (int k = 0; k < QPT; ++k) {
-                            const int mid = __builtin_amdgcn_readfirstlane(k * BLOCK + wave * 64 + 32);
-                            const int prev = __builtin_amdgcn_readlane(bprev[k], 32);
-                            c0[k] = prev >= 0 ? prev / kChunk
-                                              : static_cast<int>(static_cast<int64_t>(mid) * n2 / max(n1, 1)) / kChunk;
-                            c0[k] = min(max(c0[k], 0), nch - 1);
-                            vq[k] = k * BLOCK + tid < n1;
+                            const int i = k * BLOCK + tid;
+                            pred[k] = bprev[k] >= 0 ? bprev[k]
+                                                    : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
+                            vq[k] = i < n1;
                         }
-                        nn_scan_pruned<QPT>(candf, box, nch, fx, fy, vq, c0, M1, M2, C1, nscan_total);
+                        nn_window_pruned<QPT>(candf, box8, nsub, fx, fy, vq, pred, M1, M2, C1,
+                                              nscan_total, stamping, tsub);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
                     }
@@ -485,15 +505,18 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
                     qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));   // bit-identical to above
                     qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
                     // winning chunk: first index reaching the chunk minimum + runner-up
-                    float b1 = INFINITY, b2 = INFINITY;
+                    float b2 = INFINITY;
                     int j1 = C1[k];
+                    if constexpr (!PRUNE) {   // PRUNE tracked the exact index and runner-up already
+                        float b1 = INFINITY;
 #pragma unroll 2
-                    for (int j = C1[k]; j < C1[k] + kChunk; ++j) {
-                        const float2 p = candf[j];
-                        const float d = screen_d32(p.x, p.y, fx[k], fy[k]);
-                        b2 = __builtin_amdgcn_fmed3f(b1, b2, d);
-                        if (d < b1) j1 = j;
-                        b1 = fminf(b1, d);
+                        for (int j = C1[k]; j < C1[k] + kChunk; ++j) {
+                            const float2 p = candf[j];
+                            const float d = screen_d32(p.x, p.y, fx[k], fy[k]);
+                            b2 = __builtin_amdgcn_fmed3f(b1, b2, d);
+                            if (d < b1) j1 = j;
+                            b1 = fminf(b1, d);
+                        }
                     }
                     j1 = min(j1, n2 - 1);
                     bi[k] = j1;
@@ -585,17 +608,12 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
         }
 
         // ---- src/icp.py:64,68  centroids + error ------------------------------
-        double bx[QPT], by[QPT];
         double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
             const int i = k * BLOCK + tid;
-            bx[k] = 0.0;
-            by[k] = 0.0;
             if (i < n1) {
                 const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
-                bx[k] = m.x;
-                by[k] = m.y;
                 v[0] += qx[k];
                 v[1] += qy[k];
                 v[2] += m.x;
@@ -615,8 +633,9 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
         for (int k = 0; k < QPT; ++k) {
             const int i = k * BLOCK + tid;
             if (i < n1) {
+                const double2 m = resident ? cand[bi[k]] : p2[bi[k]];   // re-read: fewer live registers
                 const double xa = qx[k] - mux, ya = qy[k] - muy;
-                const double xb = bx[k] - mvx, yb = by[k] - mvy;
+                const double xb = m.x - mvx, yb = m.y - mvy;
                 s[0] = fma(xa, xb, s[0]);
                 s[1] = fma(xa, yb, s[1]);
                 s[2] = fma(ya, xb, s[2]);
@@ -663,7 +682,9 @@ __global__ __launch_bounds__(BLOCK) void icp_kernel(IcpArgs a) {
             const bool stop = (err < a.epsilon) || (it > a.max_iters) ||
                               (it > 0 && fabs(last_err - err) < a.stopping_thresh);
             last_err = err;
-            T = Tn;
+            // Tn is identical in every lane: keep it in SGPRs
+            T.m00 = uniform_d(Tn.m00); T.m01 = uniform_d(Tn.m01); T.m02 = uniform_d(Tn.m02);
+            T.m10 = uniform_d(Tn.m10); T.m11 = uniform_d(Tn.m11); T.m12 = uniform_d(Tn.m12);
             if (stop) {
                 flush_stamps();
                 if (tid == 0) {
@@ -695,16 +716,18 @@ struct Instance {
     KernelFn step_prune;
 };
 
-#define SLAM_INST(B, Q)                                                                   \
+// W: minimum waves per SIMD the pruned batch kernel is compiled for (4 on the
+// default 1081-point shape: 128 VGPRs, a few cold spills, +10 % measured)
+#define SLAM_INST(B, Q, W)                                                                 \
     {B, Q, icp_kernel<B, Q, false, false>, icp_kernel<B, Q, true, false>,                 \
      icp_kernel<B, Q, false, true>, icp_kernel<B, Q, true, true>,                         \
-     icp_kernel<B, Q, false, true, true>, icp_kernel<B, Q, true, true, true>}
+     icp_kernel<B, Q, false, true, true, W>, icp_kernel<B, Q, true, true, true>}
 static const Instance kInstances[] = {
-    SLAM_INST(64, 1),   SLAM_INST(64, 2),   SLAM_INST(64, 4),   SLAM_INST(128, 3),
-    SLAM_INST(128, 4),  SLAM_INST(192, 4),  SLAM_INST(192, 6),  SLAM_INST(256, 4),
-    SLAM_INST(256, 5),  SLAM_INST(320, 4),  SLAM_INST(384, 3),  SLAM_INST(512, 3),
-    SLAM_INST(576, 2),  SLAM_INST(512, 4),  SLAM_INST(512, 6),  SLAM_INST(512, 8),
-    SLAM_INST(512, 16),
+    SLAM_INST(64, 1, 1),   SLAM_INST(64, 2, 1),   SLAM_INST(64, 4, 1),   SLAM_INST(128, 3, 1),
+    SLAM_INST(128, 4, 1),  SLAM_INST(192, 4, 1),  SLAM_INST(192, 6, 1),  SLAM_INST(256, 4, 1),
+    SLAM_INST(256, 5, 4),  SLAM_INST(320, 4, 1),  SLAM_INST(384, 3, 1),  SLAM_INST(512, 3, 1),
+    SLAM_INST(576, 2, 1),  SLAM_INST(512, 4, 1),  SLAM_INST(512, 6, 1),  SLAM_INST(512, 8, 1),
+    SLAM_INST(512, 16, 1),
 };
 #undef SLAM_INST
 constexpr int kNumInstances = sizeof(kInstances) / sizeof(kInstances[0]);
@@ -803,7 +826,7 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     if (mode >= 1)
         lds += static_cast<size_t>(a.cand_cap) * sizeof(float2) +
                2 * sizeof(int) * static_cast<size_t>(inst->block) * inst->qpt;
-    if (mode == 2) lds += static_cast<size_t>(a.cand_cap / kChunk) * sizeof(float4);
+    if (mode == 2) lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4);
     KernelFn fn = mode == 2 ? (step ? inst->step_prune : inst->batch_prune)
                 : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)
                             : (step ? inst->step : inst->batch);

@@ -31,5 +31,7 @@ for n, v in zip(names, t[:4]):
     print(f"{n:22s} {v / its:10.1f} ticks/iter ({v / max(t[:4].sum(), 1) * 100:5.1f} %)")
 nch = (int(ss.lens[0]) + 31) // 32
 qpt = int(os.environ.get("QPT", "5"))
-print(f"chunks scanned per query group per iteration (wave 0): {t[4] / its / qpt:.2f} of {nch}")
+print(f"extra sub-chunks visited per query group per iteration (wave 0): {t[4] / its / qpt:.2f} of {nch * 4}")
 
+for n, v in zip(["  window scan", "  group box+mask", "  visits"], t[5:8]):
+    print(f"{n:22s} {v / its:10.1f} ticks/iter")

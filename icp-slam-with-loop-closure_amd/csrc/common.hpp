@@ -71,13 +71,32 @@ __device__ __forceinline__ SE2 se2_mul(const SE2& a, const SE2& b) {
     return c;
 }
 
-// All-lane sum of a wave64 by xor butterfly: every lane ends with the same
-// bits (each stage adds the same two operands, only commuted).
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+// All-lane sum of a wave64 without LDS: pairs and quads by DPP quad_perm,
+// quads of a 16-lane row by DPP row_ror 12 / 8 (lane 0 of each row then holds
+// the row sum), the four rows through SGPRs as (r0+r1)+(r2+r3).  Every lane
+// returns identical bits.
+#define SLAM_DPP_D(v, ctrl)                                                                            \
+    __longlong_as_double(                                                                              \
+        (static_cast<long long>(__builtin_amdgcn_update_dpp(                                           \
+             0, static_cast<int>(__double_as_longlong(v) >> 32), ctrl, 0xF, 0xF, false))                \
+         << 32) |                                                                                      \
+        static_cast<unsigned int>(__builtin_amdgcn_update_dpp(                                         \
+            0, static_cast<int>(__double_as_longlong(v) & 0xffffffff), ctrl, 0xF, 0xF, false)))
+// Lane `lane`'s double (lane wave-uniform) through SGPRs.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b & 0xffffffff), lane);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), lane);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
+__device__ __forceinline__ double wave_sum(double v) {
+    v += SLAM_DPP_D(v, 0xB1);    // xor 1
+    v += SLAM_DPP_D(v, 0x4E);    // xor 2
+    v += SLAM_DPP_D(v, 0x12C);   // row_ror 12
+    v += SLAM_DPP_D(v, 0x128);   // row_ror 8
+    return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+#undef SLAM_DPP_D
 
 // Deterministic block all-reduce of NV doubles; `red` is LDS scratch of
 // WAVES * NV doubles.  Every thread returns identical bits (fixed wave order).

@@ -39,14 +39,6 @@ constexpr int kGnContrib = 34;   // per-edge: 9 AtWA, 9 AtWB, 9 BtWB, 3 AtWe, 3 
 constexpr int kGnBlock = 512;    // threads of the factor / solve workgroup
 constexpr int kGnS = 16;         // Cholesky block size (scalar columns per step)
 
-// Broadcast lane l's double (l wave-uniform) through SGPRs (v_readlane).
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long x = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
-    const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), l);
-    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
-}
-
 __device__ __forceinline__ double wrap_pi(double a) {
     return a - 2.0 * M_PI * floor((a + M_PI) / (2.0 * M_PI));
 }

@@ -67,6 +67,10 @@ __device__ __forceinline__ double uniform_d(double v) {
     return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
+__device__ __forceinline__ float uniform_f(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 // Squared distance with NumPy's rounding: sum((pc2[j] - q)**2) over x, y (+0).
 __device__ __forceinline__ double exact_d2(double px, double py, double qx, double qy) {
     const double dx = px - qx;
@@ -203,9 +207,12 @@ __device__ __forceinline__ void scan_chunk(const float2* __restrict__ candf, int
 // Conservative squared distance between two axis-aligned boxes (or a point,
 // as a degenerate box), rounded DOWN by 1e-6 relative: a lower bound of every
 // fp32 screened distance between their points (>> the ~16 u of rounding).
-__device__ __forceinline__ float box_lb(float ax0, float ax1, float ay0, float ay1, const float4& b) {
-    const float ddx = fmaxf(fmaxf(b.x - ax1, ax0 - b.y), 0.0f);
-    const float ddy = fmaxf(fmaxf(b.z - ay1, ay0 - b.w), 0.0f);
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float box_lb(f32x2 alo, f32x2 ahi, const float4& b) {
+    const f32x2 d0 = f32x2{b.x, b.y} - ahi;   // box b = (x0, y0, x1, y1): v_pk_add_f32
+    const f32x2 d1 = alo - f32x2{b.z, b.w};
+    const float ddx = fmaxf(fmaxf(d0.x, d1.x), 0.0f);
+    const float ddy = fmaxf(fmaxf(d0.y, d1.y), 0.0f);
     return fmaf(ddy, ddy, ddx * ddx) * (1.0f - 1e-6f);
 }
 
@@ -237,10 +244,11 @@ __device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, 
 template <int QPT>
 __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ candf,
                                                  const float4* __restrict__ box8, int nsub,
+                                                 const double4* __restrict__ gbox, const SE2& T,
                                                  const float (&qx)[QPT], const float (&qy)[QPT],
                                                  const bool (&valid)[QPT], const int (&pred)[QPT],
                                                  float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
-                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[3]) {
+                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[5]) {
     const int lane = threadIdx.x & 63;
     unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
     auto lap = [&](int q) {   // diagnostics: sub-phase s_memtime (workgroup 0, wave 0)
@@ -269,13 +277,22 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     for (int k = 0; k < QPT; ++k) J1[k] += ws[k] * kSub;
     lap(0);
     // 2. group boxes and largest M2, all groups interleaved
+    // The box of a group's transformed queries is the transformed box of its
+    // original points (gbox, computed once per pair), widened by 1e-6 of the
+    // coordinate magnitude so it also holds their fp32 roundings.
     float gx0[QPT], gx1[QPT], gy0[QPT], gy1[QPT], gM2[QPT];
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-        gx0[k] = wave_min_f(valid[k] ? qx[k] : INFINITY);
-        gx1[k] = wave_max_f(valid[k] ? qx[k] : -INFINITY);
-        gy0[k] = wave_min_f(valid[k] ? qy[k] : INFINITY);
-        gy1[k] = wave_max_f(valid[k] ? qy[k] : -INFINITY);
+        const double4 g = gbox[k];   // (x0, x1, y0, y1) of the group's valid original points
+        const double ax = T.m00 * g.x, bx = T.m00 * g.y, cx = T.m01 * g.z, dx = T.m01 * g.w;
+        const double ay = T.m10 * g.x, by = T.m10 * g.y, cy = T.m11 * g.z, dy = T.m11 * g.w;
+        const double magx = fabs(T.m02) + fmax(fabs(ax), fabs(bx)) + fmax(fabs(cx), fabs(dx));
+        const double magy = fabs(T.m12) + fmax(fabs(ay), fabs(by)) + fmax(fabs(cy), fabs(dy));
+        const double ex = 1e-6 * magx + 1e-30, ey = 1e-6 * magy + 1e-30;
+        gx0[k] = uniform_f(static_cast<float>(T.m02 + fmin(ax, bx) + fmin(cx, dx) - ex));
+        gx1[k] = uniform_f(static_cast<float>(T.m02 + fmax(ax, bx) + fmax(cx, dx) + ex));
+        gy0[k] = uniform_f(static_cast<float>(T.m12 + fmin(ay, by) + fmin(cy, dy) - ey));
+        gy1[k] = uniform_f(static_cast<float>(T.m12 + fmax(ay, by) + fmax(cy, dy) + ey));
         gM2[k] = wave_max_f(valid[k] ? M2[k] : -INFINITY);
     }
     lap(1);
@@ -288,34 +305,47 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     for (int k = 0; k < QPT; ++k) {
         for (int w = 0; w < nw; ++w) {
             const int sl = 64 * w + lane;
-            uint64_t live = __ballot(sl < nsub && box_lb(gx0[k], gx1[k], gy0[k], gy1[k], box8[sl]) <= gM2[k]);
+            // branch-free (no short-circuit): the LDS reads are not serialised behind exec-mask jumps
+            const bool gl = box_lb(f32x2{gx0[k], gy0[k]}, f32x2{gx1[k], gy1[k]}, box8[min(sl, nsub - 1)]) <= gM2[k];
+            uint64_t live = __ballot((sl < nsub) & gl);
+            if (stamping) tsub[3] += __popcll(live);
             while (live) {
                 // up to kBatch live sub-chunks per batch, straight-line: the box
                 // reads (broadcast) and tests issue back to back
-                int sc[kBatch];
+                uint64_t scpack = 0;   // 6-bit in-word positions of this batch's sub-chunks
+                uint32_t has = 0;
+                float4 bb[kBatch];
+#pragma unroll
+                for (int u = 0; u < kBatch; ++u) {   // all box reads first (broadcast), then the tests
+                    const int pos = live ? static_cast<int>(__builtin_ctzll(live)) : 0;
+                    has |= static_cast<uint32_t>(live != 0) << u;
+                    live &= live - 1;
+                    scpack |= static_cast<uint64_t>(pos) << (6 * u);
+                    bb[u] = box8[64 * w + pos];
+                }
+                if (stamping) tsub[4] += 1;
                 uint32_t need = 0;
 #pragma unroll
                 for (int u = 0; u < kBatch; ++u) {
-                    const bool has = live != 0;
-                    sc[u] = has ? 64 * w + static_cast<int>(__builtin_ctzll(live | (1ull << 63))) : 0;
-                    live &= live - 1;
-                    const bool nd = has && valid[k] && (sc[u] < ws[k] || sc[u] >= ws[k] + kWin) &&
-                                    box_lb(qx[k], qx[k], qy[k], qy[k], box8[sc[u]]) <= M2[k];
+                    const int sc = 64 * w + static_cast<int>((scpack >> (6 * u)) & 63);
+                    const bool near = box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, bb[u]) <= M2[k];
+                    const bool nd = valid[k] & ((sc < ws[k]) | (sc >= ws[k] + kWin)) & near;
                     need |= static_cast<uint32_t>(nd) << u;
                 }
-                const uint32_t anyneed = wave_or_u32(need);
+                need &= has;
+                // scan the sub-chunks some lane needs (rolled loop: small code)
+                uint32_t todo = wave_or_u32(need);
+                while (todo) {
+                    const int u = __builtin_ctz(todo);
+                    todo &= todo - 1;
+                    const int c8 = (64 * w + static_cast<int>((scpack >> (6 * u)) & 63)) * kSub;
+                    ++nvisit;
+                    if ((need >> u) & 1u) {
 #pragma unroll
-                for (int u = 0; u < kBatch; ++u) {
-                    if ((anyneed >> u) & 1u) {
-                        ++nvisit;
-                        if ((need >> u) & 1u) {
-                            const int c8 = sc[u] * kSub;
-#pragma unroll
-                            for (int t = 0; t < kSub; t += 2) {
-                                const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
-                                take_cand(screen_d32(pp.x, pp.y, qx[k], qy[k]), c8 + t, M1[k], M2[k], J1[k]);
-                                take_cand(screen_d32(pp.z, pp.w, qx[k], qy[k]), c8 + t + 1, M1[k], M2[k], J1[k]);
-                            }
+                        for (int t = 0; t < kSub; t += 2) {
+                            const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
+                            take_cand(screen_d32(pp.x, pp.y, qx[k], qy[k]), c8 + t, M1[k], M2[k], J1[k]);
+                            take_cand(screen_d32(pp.z, pp.w, qx[k], qy[k]), c8 + t + 1, M1[k], M2[k], J1[k]);
                         }
                     }
                 }
@@ -325,19 +355,18 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     lap(2);
 }
 
-// Lower bound of the exact squared distance T of any candidate whose fp32
-// screened distance is >= d32 (DESIGN.md §"fp32 screen, exact answer"):
-// d32 <= F(T) = (1+8u) T + 3a sqrt(T) + 3a^2 with u = 2^-24 and a the
-// coordinate-rounding bound (1+u) u (|p|max + |q|max); T >= F^{-1}(d32).
-__device__ __forceinline__ double screen_lower_bound(double d32, double a) {
-    const double alpha = 1.0 + 8.0 * 0x1p-24;
-    const double beta = 3.0 * a;
-    const double gamma = 3.0 * a * a + 1e-37;
-    const double disc = beta * beta - 4.0 * alpha * (gamma - d32);
-    if (!(disc > 0.0)) return 0.0;
-    const double s = (-beta + sqrt(disc)) / (2.0 * alpha);
-    if (!(s > 0.0)) return 0.0;
-    return s * s * (1.0 - 1e-12);
+// Certification of a screened winner (DESIGN.md §"fp32 screen, exact answer").
+// Any candidate at exact squared distance T has screened distance
+// d32 <= F(T) = (1+8u) T + 3a sqrt(T) + 3a^2 (u = 2^-24, a = the coordinate
+// rounding bound (1+u) u (|p|max + |q|max)); F is strictly increasing.  If
+// every other candidate has d32 >= s2 and s2 > F(d1), all of them have
+// T > d1: the winner (exact distance d1) is the unique exact minimum.  Fc is
+// an upper bound of F(d1) (sqrt rounded up through fp32, 1e-12 relative slack).
+__device__ __forceinline__ bool certify(double d1, double s2, double a) {
+    const float sq = sqrtf(static_cast<float>(d1)) * (1.0f + 1e-6f) + 1e-19f;   // >= sqrt(d1)
+    const double fc = fma(1.0 + 8.0 * 0x1p-24, d1, fma(3.0 * a, static_cast<double>(sq), 3.0 * a * a)) *
+                          (1.0 + 1e-12) + 1e-37;
+    return s2 > fc;
 }
 
 template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false, int WPE = 1>
@@ -353,6 +382,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     int* fq = reinterpret_cast<int*>(candf + cap);          // [WAVES][64*QPT] query ids
     int* fres = fq + WAVES * 64 * QPT;                       // [WAVES][64*QPT] exact answers
     float4* box8 = reinterpret_cast<float4*>(fres + WAVES * 64 * QPT);   // PRUNE: [cap/8] sub-chunk boxes
+    double4* gbox = reinterpret_cast<double4*>(box8 + cap / kSub);          // PRUNE: [WAVES][QPT] query boxes
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -395,7 +425,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 y0 = fminf(y0, p.y);
                 y1 = fmaxf(y1, p.y);
             }
-            box8[c] = make_float4(x0, x1, y0, y1);
+            box8[c] = make_float4(x0, y0, x1, y1);
+        }
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {   // bounding box of each group's valid original points
+            const int i = k * BLOCK + tid;
+            double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+            if (i < n1) {
+                const double2 p = p1[i];
+                x0 = x1 = p.x;
+                y0 = y1 = p.y;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                x0 = fmin(x0, __shfl_xor(x0, off, 64));
+                x1 = fmax(x1, __shfl_xor(x1, off, 64));
+                y0 = fmin(y0, __shfl_xor(y0, off, 64));
+                y1 = fmax(y1, __shfl_xor(y1, off, 64));
+            }
+            if (lane == 0) gbox[wave * QPT + k] = make_double4(x0, x1, y0, y1);
         }
     }
     int bprev[QPT];
@@ -429,7 +477,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     __syncthreads();
 
     double last_err = 0.0;
-    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[3] = {0, 0, 0};
+    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[5] = {0, 0, 0, 0, 0};
 
     const bool stamping = a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
     auto stamp = [&](int ph) {
@@ -443,7 +491,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         if (stamping && lane == 0) {
             for (int q = 0; q < 4; ++q) a.stamps[q] = tph[q];
             a.stamps[4] = static_cast<unsigned long long>(nscan_total);   // sub-chunks visited (wave 0)
-            for (int q = 0; q < 3; ++q) a.stamps[5 + q] = tsub[q];
+            for (int q = 0; q < 5; ++q) a.stamps[5 + q] = tsub[q];
         }
     };
     stamp(-1);
@@ -484,7 +532,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                                                     : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
                             vq[k] = i < n1;
                         }
-                        nn_window_pruned<QPT>(candf, box8, nsub, fx, fy, vq, pred, M1, M2, C1,
+                        nn_window_pruned<QPT>(candf, box8, nsub, gbox + wave * QPT, T, fx, fy, vq, pred, M1, M2, C1,
                                               nscan_total, stamping, tsub);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
@@ -529,7 +577,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const double s2 = static_cast<double>(fminf(M2[k], b2));   // every other j: d32 >= s2
                         const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
                         const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
-                        ok = cq < 1e18 && s2 < 3.0e38 && screen_lower_bound(s2, ab) > d1;
+                        ok = cq < 1e18 && s2 < 3.0e38 && certify(d1, s2, ab);
                     }
                     const uint64_t fails = __ballot(!ok);
                     if (!ok) {
@@ -826,7 +874,9 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     if (mode >= 1)
         lds += static_cast<size_t>(a.cand_cap) * sizeof(float2) +
                2 * sizeof(int) * static_cast<size_t>(inst->block) * inst->qpt;
-    if (mode == 2) lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4);
+    if (mode == 2)
+        lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
+               static_cast<size_t>(inst->block / 64) * inst->qpt * sizeof(double4);
     KernelFn fn = mode == 2 ? (step ? inst->step_prune : inst->batch_prune)
                 : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)
                             : (step ? inst->step : inst->batch);

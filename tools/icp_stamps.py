@@ -17,7 +17,7 @@ ss = k.ScanSet(seq.scans)
 batch = k.IcpBatch(ss, np.arange(1, pairs + 1), np.arange(0, pairs), inits, epsilon=0.05, max_iters=100)
 _abi.lib().slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
 batch.launch()
-buf = torch.zeros(8, dtype=torch.int64, device="cuda")
+buf = torch.zeros(16, dtype=torch.int64, device="cuda")
 _abi.lib().slam_icp_set_stamps(buf.data_ptr())
 batch.launch()
 torch.cuda.synchronize()
@@ -35,3 +35,4 @@ print(f"extra sub-chunks visited per query group per iteration (wave 0): {t[4] /
 
 for n, v in zip(["  window scan", "  group box+mask", "  visits"], t[5:8]):
     print(f"{n:22s} {v / its:10.1f} ticks/iter")
+print(f"live sub-chunks per group per iteration: {t[8] / its / qpt:.2f}; test batches per group: {t[9] / its / qpt:.2f}")

@@ -15,7 +15,9 @@ SE(2) edges (the exchange step of the north star).  Per-GPU work is fixed as N
 grows ("scaling": "weak"); ``--strong`` shards one P-pair stream instead.
 
 Printed: ONE JSON line (rank 0) with the driver's contract fields plus
-``roofline`` (dominant kernel vs the fp64 VALU roofline, HBM rate beside it),
+``roofline`` (dominant kernel: the FP32 VALU roofline over the candidate
+distances it actually evaluates, the VALU issue fraction from the committed
+PMC profile, the HBM rate beside it),
 ``cpu_baseline`` (NumPy port of the reference, timed on this host) and
 secondary pose-graph numbers (``pgo``).
 """
@@ -33,9 +35,9 @@ sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
 FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (spec), MI355X_MICROARCH.md
 FP32_VALU_PEAK_TFLOPS = 157.3    # MI355X vector FP32 (spec)
 HBM_PEAK_GBPS = 8000.0
-VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9          # wave64 VALU op = 2 cycles on a SIMD-32
-INSTR_PER_EVAL = {"screen": 4.5, "exact": 9.0}  # VALU instructions per candidate
-FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add: the reference's work per candidate
+VALU_SIMDS = 256 * 4              # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9
+FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add per candidate distance
 
 
 def log(*a):
@@ -52,7 +54,7 @@ def parse():
     p.add_argument("--strong", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pgo", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=64, help="pairs in the CPU baseline sample")
+    p.add_argument("--cpu-sample", type=int, default=192, help="pairs in the CPU baseline sample")
     p.add_argument("--cpu-workers", type=int, default=16)
     p.add_argument("--instance", type=int, default=-1, help="force a kernel instance (diagnostics)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
@@ -249,20 +251,33 @@ def main():
 
     ms_per_step = dt_max / args.steps * 1e3
     value = pairs_all * args.steps / dt_max
-    # dominant kernel: slam_icp_batch_f64 on rank 0 (its own pairs)
-    screen = os.environ.get("SLAMHIP_SCREEN", "1") != "0" and int(ss.lens.max()) <= 4096
-    peak = FP32_VALU_PEAK_TFLOPS if screen else FP64_VALU_PEAK_TFLOPS
-    flops = FLOP_PER_EVAL * evals / (kern_ms * 1e-3) / 1e12
-    issue_bound = VALU_LANE_OPS / INSTR_PER_EVAL["screen" if screen else "exact"]
+    # dominant kernel: slam_icp_batch_f64 on rank 0 (its own pairs).  Work is
+    # counted as the candidate distances the kernel actually evaluates (exact
+    # pruning skips most of the n1*n2 brute-force set): one counting launch,
+    # outside the timed region (the search is deterministic).
+    mode = int(os.environ.get("SLAMHIP_SCREEN", "2")) if int(ss.lens.max()) <= 4096 else 0
+    cnt = torch.zeros(1, dtype=torch.int64, device=ss.device)
+    lib.slam_icp_set_eval_counter(cnt.data_ptr())
+    batch.launch()
+    torch.cuda.synchronize()
+    lib.slam_icp_set_eval_counter(None)
+    performed = float(cnt.item())
+    peak = FP32_VALU_PEAK_TFLOPS if mode else FP64_VALU_PEAK_TFLOPS
+    flops = FLOP_PER_EVAL * performed / (kern_ms * 1e-3) / 1e12
     alg_bytes = 16.0 * float(ss.lens.sum()) + B * (4 + 4 + 72 + 72 + 8 + 4) + 8 * (len(ss.lens) + 1)
     hbm_gbps = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
+    valu_issue = None
     tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             # measured on tj["pairs"] pairs of this workload; scale to this launch
             traffic = round(tj["icp_batch_bytes_per_launch"] * B / tj.get("pairs", B))
+            if "valu_insts_per_launch" in tj:
+                # wave64 VALU instruction = 4 cycles of a SIMD (profiles/r01_ubench_valu.txt)
+                cap = VALU_SIMDS * CLOCK_HZ * (kern_ms * 1e-3) / 4.0
+                valu_issue = round(tj["valu_insts_per_launch"] * B / tj.get("pairs", B) / cap, 4)
         except Exception:
             traffic = None
     sel = lib.slam_icp_selected_instance(int(n1.max()))
@@ -289,16 +304,20 @@ def main():
                    "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}"},
         "roofline": {
             "bound": "valu",
-            "kernel": "slam_icp_batch_f64 (icp_kernel, %s)" % ("fp32 screen + exact fp64 certification"
-                                                               if screen else "exact fp64 scan"),
+            "kernel": "slam_icp_batch_f64 (icp_kernel, %s)" % (
+                {2: "fp32 screen with exact pruning + fp64 certification",
+                 1: "fp32 screen + fp64 certification", 0: "exact fp64 scan"}[mode]),
             "achieved": round(flops, 3),
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(flops / peak, 4),
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 4),
-            "candidate_evals_per_launch": evals,
-            "issue_bound_frac": round(evals / (kern_ms * 1e-3) / issue_bound, 4),
+            "candidate_evals_performed_per_launch": performed,
+            "brute_force_evals_per_launch": evals,
+            "pruning_factor": round(evals / max(performed, 1.0), 2),
+            "brute_force_equivalent_evals_per_s": round(evals / (kern_ms * 1e-3), 1),
+            "valu_issue_frac": valu_issue,
             "hbm": {"achieved": round(hbm_gbps, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 6), "algorithmic_bytes_per_launch": alg_bytes},
         },

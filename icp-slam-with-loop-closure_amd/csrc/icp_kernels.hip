@@ -57,6 +57,8 @@ struct IcpArgs {
     const int64_t* corr_off;
     // diagnostics: per-phase s_memtime totals of workgroup 0 (NULL = off)
     unsigned long long* stamps;
+    // diagnostics: total candidate evaluations performed, all lanes (NULL = off)
+    unsigned long long* evals;
 };
 
 // A wave-uniform double moved to SGPRs (v_readfirstlane of both halves).
@@ -248,7 +250,8 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                                                  const float (&qx)[QPT], const float (&qy)[QPT],
                                                  const bool (&valid)[QPT], const int (&pred)[QPT],
                                                  float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
-                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[5]) {
+                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[5],
+                                                 bool counting, unsigned long long& nev) {
     const int lane = threadIdx.x & 63;
     unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
     auto lap = [&](int q) {   // diagnostics: sub-phase s_memtime (workgroup 0, wave 0)
@@ -275,6 +278,10 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     }
 #pragma unroll
     for (int k = 0; k < QPT; ++k) J1[k] += ws[k] * kSub;
+    if (counting) {
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) nev += kWin * kSub * __popcll(__ballot(valid[k]));
+    }
     lap(0);
     // 2. group boxes and largest M2, all groups interleaved
     // The box of a group's transformed queries is the transformed box of its
@@ -340,6 +347,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                     todo &= todo - 1;
                     const int c8 = (64 * w + static_cast<int>((scpack >> (6 * u)) & 63)) * kSub;
                     ++nvisit;
+                    if (counting) nev += kSub * __popcll(__ballot((need >> u) & 1u));
                     if ((need >> u) & 1u) {
 #pragma unroll
                         for (int t = 0; t < kSub; t += 2) {
@@ -387,7 +395,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
     const int s1 = a.src_scan[b];
     const int s2 = a.dst_scan[b];
     const int64_t o1 = a.scan_off[s1];
@@ -461,6 +469,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         cmax = red1[0];
 #pragma unroll
         for (int w = 1; w < WAVES; ++w) cmax = fmax(cmax, red1[w]);
+        cmax = uniform_d(cmax);
         screen = cmax < 1e18;   // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
     }
     const int n2_pad = (n2 + kChunk - 1) / kChunk * kChunk;
@@ -480,6 +489,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[5] = {0, 0, 0, 0, 0};
 
     const bool stamping = a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
+    const bool counting = a.evals != nullptr;
+    unsigned long long nev = 0;
     auto stamp = [&](int ph) {
         if (stamping) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -496,7 +507,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     };
     stamp(-1);
     for (int it = 0;; ++it) {
-        asm volatile("" ::: "memory");   // keep pc1 re-loads inside the loop (registers, not LICM)
+        // An opaque copy of the thread index per iteration: query addresses and
+        // masks derived from it are recomputed (2 VALU) instead of hoisted out
+        // of the loop and spilled to scratch.
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
         double qx[QPT], qy[QPT];
         int bi[QPT];
         if constexpr (SCREEN) {
@@ -533,9 +548,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                             vq[k] = i < n1;
                         }
                         nn_window_pruned<QPT>(candf, box8, nsub, gbox + wave * QPT, T, fx, fy, vq, pred, M1, M2, C1,
-                                              nscan_total, stamping, tsub);
+                                              nscan_total, stamping, tsub, counting, nev);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
+                        if (counting) {   // full screen + winning-chunk rescan
+#pragma unroll
+                            for (int k = 0; k < QPT; ++k)
+                                nev += (n2_pad + kChunk) * __popcll(__ballot(k * BLOCK + tid < n1));
+                        }
                     }
                 }
                 stamp(0);
@@ -588,6 +608,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         bi[k] = -1 - pos;   // resolved below
                     }
                     base += __popcll(fails);
+                    if (counting) nev += static_cast<unsigned long long>(n2) * __popcll(fails);   // exact fallback
                 }
                 stamp(1);
                 // ---- wave-cooperative exact fallback for uncertified queries ---
@@ -644,6 +665,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
             if (resident) {
                 nn_scan_f64<QPT>(cand, n2, 0, qx, qy, best, bi);
+                if (counting) {
+#pragma unroll
+                    for (int k = 0; k < QPT; ++k) nev += static_cast<unsigned long long>(n2) * __popcll(__ballot(k * BLOCK + tid < n1));
+                }
             } else {
                 for (int t0 = 0; t0 < n2; t0 += cap) {
                     const int cnt = min(cap, n2 - t0);
@@ -651,6 +676,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     for (int j = tid; j < cnt; j += BLOCK) cand[j] = p2[t0 + j];
                     __syncthreads();
                     nn_scan_f64<QPT>(cand, cnt, t0, qx, qy, best, bi);
+                    if (counting) {
+#pragma unroll
+                        for (int k = 0; k < QPT; ++k) nev += static_cast<unsigned long long>(cnt) * __popcll(__ballot(k * BLOCK + tid < n1));
+                    }
                 }
             }
         }
@@ -717,6 +746,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                 a.out_err[b] = err;
             }
+            if (counting && lane == 0) atomicAdd(a.evals, nev);
             int64_t* corr = a.out_corr + a.corr_off[b];
 #pragma unroll
             for (int k = 0; k < QPT; ++k) {
@@ -735,6 +765,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             T.m10 = uniform_d(Tn.m10); T.m11 = uniform_d(Tn.m11); T.m12 = uniform_d(Tn.m12);
             if (stop) {
                 flush_stamps();
+                if (counting && lane == 0) atomicAdd(a.evals, nev);
                 if (tid == 0) {
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
@@ -861,6 +892,7 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
 // three (tests/test_icp_gpu.py::test_nn_modes_identical).
 static int g_screen = 2;
 static unsigned long long* g_icp_stamps = nullptr;
+static unsigned long long* g_icp_evals = nullptr;
 
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
                   void* stream) {
@@ -868,6 +900,7 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     if (!inst) return fail(SLAM_ETOOBIG, "query scan of %d points exceeds capacity %d", max_n1, kMaxQuery);
     IcpArgs a = args;
     a.stamps = g_icp_stamps;
+    a.evals = g_icp_evals;
     a.cand_cap = max_n2 < kCandCap ? ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk : kCandCap;
     const int mode = max_n2 <= kCandCap ? g_screen : 0;
     size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
@@ -913,6 +946,10 @@ int slam_icp_force_instance(int i) {
 }
 int slam_icp_set_stamps(void* dev_buf) {
     g_icp_stamps = reinterpret_cast<unsigned long long*>(dev_buf);
+    return ok();
+}
+int slam_icp_set_eval_counter(void* dev_u64) {
+    g_icp_evals = reinterpret_cast<unsigned long long*>(dev_u64);
     return ok();
 }
 int slam_icp_set_screen(int mode) {

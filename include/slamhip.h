@@ -160,10 +160,14 @@ int slam_icp_instance_shape(int i, int* block, int* qpt);
 int slam_icp_force_instance(int i);
 int slam_icp_selected_instance(int max_n1);
 /* NN search mode: 0 exact fp64 scan, 1 fp32 screen (all chunks), 2 fp32
- * screen with exact chunk pruning (default); identical results. */
+ * screen with exact pruning (per-lane windows + sub-chunk boxes, default);
+ * identical results. */
 int slam_icp_set_screen(int mode);
 int slam_gn_set_stamps(void* dev_buf);
 int slam_icp_set_stamps(void* dev_buf);
+/* Count candidate-distance evaluations performed (all lanes) into a device
+ * uint64 (atomic add per wave); NULL turns counting off. */
+int slam_icp_set_eval_counter(void* dev_u64);
 
 #ifdef __cplusplus
 }

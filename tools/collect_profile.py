@@ -20,12 +20,16 @@ def main(tag):
     shutil.copy(os.path.join(src, "trace", "icp_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     vals = {}
     rows_out = []
-    for name, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+    for names, sub in ((("FETCH_SIZE",), "pmc_fetch"), (("WRITE_SIZE",), "pmc_write"),
+                       (("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"), "pmc_inst")):
         d = os.path.join(src, sub)
+        if not os.path.isdir(d):
+            continue
         f = [x for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
         for r in csv.DictReader(open(os.path.join(d, f))):
-            if "icp_kernel" in r["Kernel_Name"] and r["Counter_Name"] == name:
-                vals[name] = float(r["Counter_Value"])
+            if "icp_kernel" in r["Kernel_Name"] and r["Counter_Name"] in names:
+                name = r["Counter_Name"]
+                vals[name] = vals.get(name, 0.0) + float(r["Counter_Value"])
                 rows_out.append({k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                                    "VGPR_Count", "SGPR_Count", "Counter_Name", "Counter_Value")})
     with open(os.path.join(dst, f"{tag}_pmc_icp.csv"), "w", newline="") as f:
@@ -39,6 +43,11 @@ def main(tag):
            "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one launch", "pairs": 10000,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
            "tag": tag}
+    if "SQ_INSTS_VALU" in vals:
+        out.update({"valu_insts_per_launch": vals["SQ_INSTS_VALU"], "salu_insts_per_launch": vals["SQ_INSTS_SALU"],
+                    "lds_insts_per_launch": vals["SQ_INSTS_LDS"], "waves_per_launch": vals["SQ_WAVES"],
+                    "inst_method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES (wave-level "
+                                   "instruction counts, summed over the launch)"})
     json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -2,7 +2,8 @@
 # Round profiling recipe (run on the GPU box from the repo root):
 #   kernel trace + stats of the bench, then FETCH_SIZE and WRITE_SIZE in
 #   separate PMC passes (MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE need
-#   separate passes; FETCH_SIZE under-reports wide coalesced reads by 2x).
+#   separate passes; FETCH_SIZE under-reports wide coalesced reads by 2x), then
+#   the instruction mix (VALU / SALU / LDS instructions, waves).
 set -e
 TAG=${1:-r01}
 export TMPDIR=/tmp
@@ -14,4 +15,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fet
     python3 tools/prof_icp.py 10000 1 > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o w -- \
     python3 tools/prof_icp.py 10000 1 > $OUT/pmc_write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d $OUT/pmc_inst -o i -- \
+    python3 tools/prof_icp.py 10000 1 > $OUT/pmc_inst.log 2>&1
 find $OUT -name "*.csv" | head -20

@@ -7,11 +7,13 @@
 //   reference                               here
 //   src/icp.py:62   np.dot(T, pc1.T).T      transform_queries(): FMA chain in
 //                                           OpenBLAS dgemm order (bit-equal)
-//   src/icp.py:4-19 get_correspondences     nn_scan(): exact fp64 distance
-//                                           (dx*dx + dy*dy, no contraction),
-//                                           strict-< ascending scan = np.argmin
-//                                           first-minimum rule; pc2 resident in
-//                                           LDS, read as broadcast ds_read_b128
+//   src/icp.py:4-19 get_correspondences     exact fp64 argmin (dx*dx + dy*dy, no
+//                                           contraction, np.argmin first-minimum
+//                                           rule), found by an fp32 screen with
+//                                           exact pruning (nn_window_pruned) and
+//                                           certified in fp64 (certify), or by the
+//                                           exhaustive fp64 scan (nn_scan_f64);
+//                                           pc2 resident in LDS
 //   src/icp.py:22-46 get_transform          two deterministic block reductions
 //                                           (centroids, then the centred 2x2
 //                                           cross-covariance) + closed-form 2x2
@@ -21,8 +23,8 @@
 //                                           identically by every thread
 //
 // Compile with -ffp-contract=off: the distance must round exactly like NumPy.
-// MFMA is deliberately not used: the work is a min-reduction, not a
-// contraction, and is bound by fp64 VALU issue.
+// MFMA is deliberately not used: the work is a min-search, not a contraction;
+// the kernel is VALU-issue / latency bound (DESIGN.md §3.1 Roofline).
 
 #include <hip/hip_runtime.h>
 
@@ -139,13 +141,6 @@ __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf
     }
 }
 
-// Exact pruning of the chunked screen (PRUNE): one query per lane, chunks
-// visited outward from c0 (the chunk of the previous iteration's match of the
-// group's middle query), and a chunk is skipped when, for EVERY lane of the
-// wave, a conservative lower bound of its fp32 distances to the chunk's
-// bounding box exceeds the lane's current second-smallest chunk minimum M2.
-// Such a chunk cannot change (M1, M2) — both only ever decrease — nor C1
-// (strict < M1), so the result equals the full scan's.
 // Wave-wide min / max without LDS: DPP butterflies inside each 16-lane row,
 // then the four row results through SGPRs (v_readlane).
 #define SLAM_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
@@ -363,7 +358,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     lap(2);
 }
 
-// Certification of a screened winner (DESIGN.md §"fp32 screen, exact answer").
+// Certification of a screened winner.
 // Any candidate at exact squared distance T has screened distance
 // d32 <= F(T) = (1+8u) T + 3a sqrt(T) + 3a^2 (u = 2^-24, a = the coordinate
 // rounding bound (1+u) u (|p|max + |q|max)); F is strictly increasing.  If

@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kGnFBlock) void gn_factor_kernel(const double* __re
             if (sb2 > 0) {
                 for (int e = lane; e < kGnS * kGnS; e += 64) {
                     const int i = e >> 4, j = e & (kGnS - 1);
-                    if (i < sb2 && j <= i) {
+                    if (i < sb2 && i < n && j <= i) {   // rows >= n have no coupling to this block (W < S)
                         double acc = 0.0;
 #pragma unroll
                         for (int t = 0; t < kGnS; ++t) acc = fma(Lp[t * LPW + i], Lp[t * LPW + j], acc);

@@ -237,3 +237,59 @@ def lap_graph_c4(seed=0, poses_per_side=125, num_loops=10, side_len=3.0, n_loops
         eb.append(b)
         tf.append(mat(rel(truth[a], truth[b])))
     return guess, np.array(ea), np.array(eb), np.stack(tf), truth
+
+
+@dataclass
+class LoopSequence(Sequence):
+    per_lap: int = 0
+    loop_pairs: np.ndarray = None   # (L, 2) ground-truth (earlier, later) scan pairs at the same lap position
+
+
+def make_loop_sequence(n_scans: int, seed: int, n_beams=N_BEAMS, step=0.05, loop_every=10,
+                       inset=1.2, lap_jitter=0.04) -> LoopSequence:
+    """Config C5 stand-in: an indoor loop — the robot drives
+    laps of a rectangle inset ``inset`` m from the walls of the same 10 x 8 m
+    room (obstacles kept in the middle, off the path), each lap shifted by a
+    small random lateral offset.  Scans at the same lap position on successive
+    laps form the ground-truth loop pairs (every ``loop_every``-th position),
+    which the manual loop-closure path (scripts/main.py:298-307) consumes
+    instead of the OpenCV image matcher."""
+    rng = np.random.default_rng(seed)
+    width, height = 10.0, 8.0
+    obs = []
+    while len(obs) < 3:   # obstacles in the central region, clear of the loop
+        h = rng.uniform(0.3, 0.5)
+        cx = rng.uniform(inset + 1.5, width - inset - 1.5)
+        cy = rng.uniform(inset + 1.3, height - inset - 1.3)
+        if all(max(abs(cx - o[0]), abs(cy - o[1])) > h + o[2] + 0.5 for o in obs):
+            obs.append((cx, cy, h))
+    world = World(width, height, np.asarray(obs, dtype=np.float64))
+    lx, ly = width - 2 * inset, height - 2 * inset
+    perim = 2 * (lx + ly)
+    per_lap = int(round(perim / step))
+    s = np.arange(n_scans, dtype=np.float64) * step
+    lap = (s // perim).astype(np.int64)
+    u = np.mod(s, perim)
+    n_laps = int(lap.max()) + 1
+    off = rng.normal(0.0, lap_jitter, size=n_laps)[lap]          # per-lap lateral offset
+    x = np.empty(n_scans)
+    y = np.empty(n_scans)
+    th = np.empty(n_scans)
+    e1, e2, e3 = lx, lx + ly, 2 * lx + ly
+    seg = np.select([u < e1, u < e2, u < e3], [0, 1, 2], 3)
+    # counter-clockwise: bottom (+x), right (+y), top (-x), left (-y); offset pushes inward
+    x = np.where(seg == 0, inset + u, np.where(seg == 1, width - inset - off,
+                 np.where(seg == 2, width - inset - (u - e2), inset + off)))
+    y = np.where(seg == 0, inset + off, np.where(seg == 1, inset + (u - e1),
+                 np.where(seg == 2, height - inset - off, height - inset - (u - e3))))
+    th = np.select([seg == 0, seg == 1, seg == 2], [0.0, 0.5 * np.pi, np.pi], -0.5 * np.pi)
+    th = th + rng.normal(0.0, 0.01, size=n_scans)
+    th = np.arctan2(np.sin(th), np.cos(th))
+    truth = np.stack([x, y, th], axis=1)
+    odom = truth.copy()
+    odom[:, 0:2] += rng.normal(0.0, 0.01, size=(n_scans, 2))
+    odom[:, 2] += rng.normal(0.0, 0.005, size=n_scans)
+    scans = scans_from_poses(world, truth, rng, n_beams=n_beams)
+    later = np.arange(per_lap, n_scans, loop_every)
+    pairs = np.stack([later - per_lap, later], axis=1) if len(later) else np.zeros((0, 2), np.int64)
+    return LoopSequence(world, truth, odom, scans, per_lap=per_lap, loop_pairs=pairs.astype(np.int64))

@@ -129,3 +129,23 @@ def test_optimize_pose_graph_dropin():
     assert pg.poses is obj
     assert np.allclose(chis, ref_chi, rtol=1e-8)
     assert np.abs(pg.poses[:, :2] - ref[:, :2]).max() <= 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes", [40, 600])
+def test_gn_narrow_band(n_nodes):
+    """Bands narrower than the 16-column Cholesky block (W < S): pure chains
+    (W = 5) and a loop sequence whose RCM order folds the ring (W = 14) — the
+    look-ahead must not read panel rows beyond the band."""
+    from slamhip import gn, synthetic
+    import src.pose_graph as pgm
+    s = synthetic.make_loop_sequence(n_nodes, seed=4)
+    pg = pgm.PoseGraph(s.odometry.copy())
+    for i, j in s.loop_pairs:
+        pg.add_constraint(int(i), int(j), np.eye(3))
+    ea, eb, tf = pg.edge_arrays()
+    assert gn.GnPlan(n_nodes, ea, eb).W < 16
+    ref, ref_chi = go.optimize(s.odometry.copy(), ea, eb, tf, iterations=3)
+    got, chi = gn.optimize(s.odometry.copy(), ea, eb, tf, iterations=3)
+    assert np.allclose(chi, ref_chi, rtol=1e-8)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8

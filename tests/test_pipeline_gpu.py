@@ -1,0 +1,104 @@
+"""GPU parity of the batched driver (slamhip.pipeline, scripts/main_batched.py)
+against the reference's flow restated with the CPU oracle:
+
+* stage 1 (scripts/main.py:236-256): per-pair icp() + the serial chain —
+  corrected poses within 1e-9 (north star: 1e-5);
+* stage 2 manual path (:298-307): accepted loop closures and their
+  transforms identical in set and order, transforms within 1e-9;
+* stage 3 (:322-334): 50 SGD steps (lr = 1/(k+1)) + orientation recompute,
+  positions within 1e-9, headings modulo 2 pi.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG, homog
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+sys.path.insert(0, os.path.join(PKG, "scripts"))
+
+
+def _wrap(a):
+    return (np.asarray(a) + np.pi) % (2 * np.pi) - np.pi
+
+
+def _oracle_chain(odometry, scans, max_iters=100, eps=0.05):
+    import icp_oracle
+    from slamhip import se2
+    tfs = []
+    for i in range(1, len(odometry)):
+        h, _ = icp_oracle.icp(homog(scans[i]), homog(scans[i - 1]), se2.pose_to_mat(odometry[i] - odometry[i - 1]),
+                              eps, max_iters)
+        tfs.append(h[-1])
+    out = np.zeros((len(odometry), 3))
+    out[0] = odometry[0]
+    for i in range(1, len(odometry)):
+        out[i] = se2.mat_to_pose(se2.pose_to_mat(out[i - 1]) @ tfs[i - 1])
+    return out
+
+
+def test_stage1_scan_matching_vs_oracle():
+    from slamhip import pipeline, synthetic
+    seq = synthetic.make_sequence(25, seed=3)
+    r = pipeline.scan_matching(seq.odometry, seq.scans)
+    ref = _oracle_chain(seq.odometry, seq.scans)
+    assert np.abs(r.poses - ref).max() <= TOL
+
+
+def test_stage2_manual_loop_closures_vs_oracle():
+    import icp_oracle
+    import src.pose_graph as pgm
+    from slamhip import pipeline, synthetic
+    s = synthetic.make_loop_sequence(700, seed=2)
+    pairs = np.concatenate([s.loop_pairs[:12], [[5, 400]]])      # a far pair that ICP must reject
+    pg = pgm.PoseGraph(s.odometry.copy())
+    ok = pipeline.manual_loop_closures(pg, s.scans, pairs)
+    pg_ref = pgm.PoseGraph(s.odometry.copy())
+    for i, j in pairs:
+        h, e = icp_oracle.icp(homog(s.scans[i]), homog(s.scans[j]), np.eye(3), 0.05, 100)
+        if e < 30:
+            pg_ref.add_constraint(int(i), int(j), h[-1])
+    ea, eb, tf = pg.edge_arrays()
+    ra, rb, rtf = pg_ref.edge_arrays()
+    assert np.array_equal(ea, ra) and np.array_equal(eb, rb)
+    assert np.abs(tf - rtf).max() <= TOL
+    assert ok[:12].sum() >= 10 and not ok[-1]
+
+
+def test_stage3_sgd_and_orientation_vs_oracle():
+    import pgo_oracle as po
+    import src.pose_graph as pgm
+    from slamhip import pipeline, synthetic
+    s = synthetic.make_loop_sequence(700, seed=2)
+    pg = pgm.PoseGraph(s.odometry.copy())
+    for i, j in s.loop_pairs[:15]:
+        pg.add_constraint(int(i), int(j), np.eye(3))
+    ea, eb, tf = pg.edge_arrays()
+    ref = s.odometry.copy()
+    for k in range(50):
+        ref = po.sgd_step(ref, ea, eb, tf, learning_rate=1 / float(k + 1))
+    ref = po.orient_from_positions(ref)
+    pipeline.optimize(pg, s.scans, optimization_max_iters=50)
+    assert np.abs(pg.poses[:, :2] - ref[:, :2]).max() <= TOL
+    assert np.abs(_wrap(pg.poses[:, 2] - ref[:, 2])).max() <= TOL
+
+
+def test_cli_end_to_end(tmp_path):
+    import main_batched as mb
+    import src.pose_graph as pgm
+    rep = mb.run(mb.parse(["synthetic:loop:600:4", "--manual-loop-closures", "auto",
+                           "--results-dir", str(tmp_path), "--optimization-max-iters", "5"]))
+    assert rep["scans"] == 600 and rep["loop_closures"]["accepted"] >= 1
+    for f in ("icp_pose_graph", "loop_closure_pose_graph", "optim"):
+        assert (tmp_path / (f + ".pickle")).exists() and (tmp_path / (f + ".g2o")).exists()
+    pg = pgm.PoseGraph(None)
+    pg.load(str(tmp_path / "optim.pickle"))
+    assert pg.poses.shape == (600, 3) and np.isfinite(pg.poses).all()
+    # restart from the saved loop-closure graph at the optimisation stage
+    rep2 = mb.run(mb.parse(["synthetic:loop:600:4", "--program-start", "optimization", "--pose-graph",
+                            str(tmp_path / "loop_closure_pose_graph.pickle"), "--results-dir", str(tmp_path),
+                            "--optimizer", "gn", "--gn-iterations", "3"]))
+    assert "optimization_s" in rep2

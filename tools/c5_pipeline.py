@@ -1,0 +1,99 @@
+"""Config C5 stand-in (BASELINE.json configs[4]): full pipeline on a
+50,000-scan synthetic indoor loop — stage 1 batched ICP odometry, ground-truth
+loop pairs through the manual loop-closure path (scripts/main.py:298-307, one
+batched ICP launch), 50 SGD steps + orientation recompute — timed per stage on
+one MI355X, with bounded CPU-reference checks (the full CPU flow would take
+hours): oracle ICP on a sample of stage-1 and loop pairs, and the first SGD
+steps on the full graph.  GPU only.  Prints one JSON line.
+
+    python tools/c5_pipeline.py [n_scans] [sgd_check_steps]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "icp-slam-with-loop-closure_amd"), os.path.join(REPO, "oracle")]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
+    sgd_check = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    import torch
+    import icp_oracle
+    import pgo_oracle as po
+    import src.pose_graph as pgm
+    from slamhip import icp as k
+    from slamhip import pgo, pipeline, se2, synthetic
+    t0 = time.perf_counter()
+    seq = synthetic.make_loop_sequence(n, seed=7)
+    t_gen = time.perf_counter() - t0
+    print(f"generated {n} scans in {t_gen:.1f}s", file=sys.stderr, flush=True)
+    rep = {"config": "C5 stand-in: synthetic indoor loop (seed 7), ground-truth manual loop closures",
+           "scans": n, "per_lap": seq.per_lap, "loop_pairs": int(len(seq.loop_pairs))}
+    pipeline.scan_matching(seq.odometry[:3], seq.scans[:3])     # warm-up
+    torch.cuda.synchronize()
+
+    t0 = time.perf_counter()
+    ss = k.ScanSet(seq.scans)
+    torch.cuda.synchronize()
+    rep["upload_s"] = round(time.perf_counter() - t0, 3)
+    t0 = time.perf_counter()
+    r1 = pipeline.scan_matching(seq.odometry, seq.scans, scanset=ss)
+    rep["stage1_scan_matching_s"] = round(time.perf_counter() - t0, 3)
+    pg = pgm.PoseGraph(r1.poses)
+    t0 = time.perf_counter()
+    ok = pipeline.manual_loop_closures(pg, seq.scans, seq.loop_pairs, scanset=ss)
+    rep["stage2_loop_closures_s"] = round(time.perf_counter() - t0, 3)
+    rep["loop_closures_accepted"] = int(ok.sum())
+    ea, eb, tf = pg.edge_arrays()
+    rep["graph"] = f"{len(pg.poses)} nodes / {len(ea)} edges"
+    poses0 = pg.poses.copy()
+    t0 = time.perf_counter()
+    solver = pgo.SgdSolver(pg.poses, ea, eb, tf)
+    for it in range(50):
+        solver.step(1.0 / float(it + 1))
+    solver.orient()
+    final = solver.host_poses()
+    rep["stage3_sgd50_orient_s"] = round(time.perf_counter() - t0, 3)
+    rep["drift_vs_truth_before_m"] = float(np.abs(r1.poses[:, :2] - seq.truth[:, :2]).max())
+    rep["drift_vs_truth_after_m"] = float(np.abs(final[:, :2] - seq.truth[:, :2]).max())
+
+    # bounded CPU-reference checks
+    rng = np.random.default_rng(0)
+    idx = rng.choice(np.arange(1, n), 24, replace=False)
+    d1 = 0.0
+    for i in idx:
+        h, _ = icp_oracle.icp(np.c_[seq.scans[i], np.ones(len(seq.scans[i]))],
+                              np.c_[seq.scans[i - 1], np.ones(len(seq.scans[i - 1]))],
+                              se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]), 0.05, 100)
+        d1 = max(d1, float(np.abs(h[-1] - r1.tf[i - 1]).max()))
+    rep["check_stage1_pairs"] = {"sampled": len(idx), "max_abs_tf_diff": d1}
+    res2 = k.icp_batch(ss, seq.loop_pairs[:16, 0], seq.loop_pairs[:16, 1],
+                       np.broadcast_to(np.eye(3), (16, 3, 3)), epsilon=0.05, max_iters=100)
+    d2 = 0.0
+    for q, (i, j) in enumerate(seq.loop_pairs[:16]):
+        h, _ = icp_oracle.icp(np.c_[seq.scans[i], np.ones(len(seq.scans[i]))],
+                              np.c_[seq.scans[j], np.ones(len(seq.scans[j]))], np.eye(3), 0.05, 100)
+        d2 = max(d2, float(np.abs(h[-1] - res2.tf[q]).max()))
+    rep["check_loop_pairs"] = {"sampled": 16, "max_abs_tf_diff": d2}
+    t0 = time.perf_counter()
+    ref = poses0.copy()
+    for it in range(sgd_check):
+        ref = po.sgd_step(ref, ea, eb, tf, learning_rate=1.0 / float(it + 1))
+    t_cpu = time.perf_counter() - t0
+    s2 = pgo.SgdSolver(poses0, ea, eb, tf)
+    for it in range(sgd_check):
+        s2.step(1.0 / float(it + 1))
+    got = s2.host_poses()
+    rep["check_sgd"] = {"steps": sgd_check, "max_abs_xy_diff": float(np.abs(got[:, :2] - ref[:, :2]).max()),
+                        "cpu_s_per_step": round(t_cpu / max(sgd_check, 1), 2),
+                        "cpu_note": "oracle/pgo_oracle.py (vectorised NumPy restatement, bit-exact with the reference)"}
+    print(json.dumps(rep))
+
+
+if __name__ == "__main__":
+    main()

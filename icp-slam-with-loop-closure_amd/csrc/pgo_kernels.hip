@@ -8,17 +8,19 @@
 //                      (one thread per node, so every M[i] is the reference's
 //                      sequential sum), W_e = inv(R sigma R^T); gamma = the
 //                      first minimum-norm diag(W_e) (sgd_gamma_kernel).
-//     pass 2 (:27-49)  sgd_relax_kernel: ONE persistent workgroup walks the
-//                      loop edges in networkx order (each edge reads poses the
-//                      previous edges moved — a true sequential dependency) and
-//                      spreads the residual over (a, b] with a block-wide
-//                      prefix sum of 1/M; the tail i > b moves by beta.
+//     pass 2 (:27-49)  sgd_prefix_kernel: prefix sums C of 1/M (pose-independent
+//                      within a step); sgd_relax_kernel: ONE persistent workgroup
+//                      walks the loop edges in networkx order (each edge reads
+//                      poses the previous edges moved — a true sequential
+//                      dependency), ramps (a, b] by C differences and moves the
+//                      tail i > b by beta through lazy per-block offsets.
 //   recompute_pose_graph_orientation (:51-57)  orient_kernel.
 //
 // Rounding: the per-edge residual, d = 2 inv(R^T sigma R) r and the clamp are
-// evaluated like the reference; the range sums use a deterministic block scan
-// instead of the reference's left-to-right loop, so poses agree to rounding
-// (tests: 1e-9 on positions after 20 steps of the reference's lap graph).
+// evaluated like the reference; the ramp uses prefix-sum differences and the
+// tail shifts are summed per block instead of the reference's left-to-right
+// running sums, so poses agree to rounding (tests: 1e-9 on positions after 20
+// steps of the reference's lap graph).
 
 #include <hip/hip_runtime.h>
 
@@ -183,23 +185,133 @@ __global__ void sgd_weights_kernel(int32_t N, const int32_t* __restrict__ ea,
 
 constexpr int kRelaxBlock = 512;
 
-// Pass 2: one workgroup, sequential over edges.  Poses live in LDS when they
-// fit (N <= kLdsPoses), otherwise in global memory (one CU: workgroup-scope
-// barriers order them).
+// Inclusive prefix sums of 1/M per column: C[0] = 0, C[i+1] = C[i] + invM[i].
+// One workgroup, chunked block scan (fixed order).  The relaxation then reads
+// the ramp sum over (a, i] as C[i+1] - C[a+1] instead of scanning per edge.
+__global__ __launch_bounds__(kRelaxBlock) void sgd_prefix_kernel(const double* __restrict__ invM, int32_t N,
+                                                                 double* __restrict__ C) {
+    constexpr int WAVES = kRelaxBlock / 64;
+    __shared__ double red[WAVES][3];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int chunk = (N + kRelaxBlock - 1) / kRelaxBlock;
+    const int lo = tid * chunk, hi = min(lo + chunk, N);
+    // 1/M is +inf for nodes no loop edge covers (M = 0); they lie in no ramp
+    // range (a, b], so they contribute 0 to the prefix.
+    auto w = [&](int i, int j) { const double v = invM[3 * i + j]; return isfinite(v) ? v : 0.0; };
+    double loc[3] = {0.0, 0.0, 0.0};
+    for (int i = lo; i < hi; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) loc[j] += w(i, j);
+    double inc[3] = {loc[0], loc[1], loc[2]};
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double o = __shfl_up(inc[j], off, 64);
+            if (lane >= off) inc[j] = o + inc[j];
+        }
+    if (lane == 63)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) red[wave][j] = inc[j];
+    __syncthreads();
+    double run[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double w0 = 0.0;
+        for (int q = 0; q < wave; ++q) w0 += red[q][j];
+        run[j] = w0 + (inc[j] - loc[j]);
+    }
+    if (tid == 0)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[j] = 0.0;
+    for (int i = lo; i < hi; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            run[j] += w(i, j);
+            C[3 * (i + 1) + j] = run[j];
+        }
+}
+
+// Active loop edges (|a - b| != 1 and a < b: the edges pass 2 applies) in
+// networkx order, compacted into (A, B, TF) so the relaxation walks only them
+// with one level of dependent loads.  One workgroup, ordered ballot compaction.
+__global__ __launch_bounds__(1024) void sgd_compact_kernel(const int32_t* __restrict__ ea,
+                                                           const int32_t* __restrict__ eb,
+                                                           const double* __restrict__ tf, int32_t E,
+                                                           int32_t* __restrict__ A, int32_t* __restrict__ B,
+                                                           double* __restrict__ TF, int32_t* __restrict__ K) {
+    __shared__ int wcount[16];
+    __shared__ int base;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    for (int e0 = 0; e0 < E; e0 += 1024) {
+        const int e = e0 + tid;
+        int a = 0, b = 0;
+        bool act = false;
+        if (e < E) {
+            a = ea[e];
+            b = eb[e];
+            act = is_loop_edge(a, b) && a < b;
+        }
+        const uint64_t m = __ballot(act);
+        const int pos_w = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                           __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+        if (lane == 0) wcount[wave] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wave; ++w) off += wcount[w];
+        if (act) {
+            const int k = off + pos_w;
+            A[k] = a;
+            B[k] = b;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) TF[9 * static_cast<int64_t>(k) + q] = tf[9 * static_cast<int64_t>(e) + q];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int w = 0; w < 16; ++w) t += wcount[w];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *K = base;
+}
+
+// Pass 2: one workgroup, sequential over the active loop edges.  Poses live in
+// LDS when they fit (N <= kLdsPoses), otherwise in global memory (one CU:
+// workgroup-scope barriers order them).  An edge (a, b) moves node i by
+//   beta (C[i+1] - C[a+1]) / tw   for a < i <= b   (the ramp, C = prefix of 1/M)
+//   beta                          for i > b        (the tail).
+// Nodes are grouped in blocks of 2^sh; only the remainder of a's block and
+// b's block are updated explicitly (<= 2^(sh+1) nodes, one per thread).  Whole
+// blocks inside (a, b) take the ramp lazily as coefficients of C
+// (cA[q] += beta/tw, off[q] -= beta C[a+1]/tw) and whole blocks after b the tail
+// (off[q] += beta), so that a node's pose is
+//   P[i] = stored[i] + off[q] + cA[q] C[i+1],   q = i >> sh,
+// and an edge costs O(2^sh + N / 2^sh) parallel work and ONE barrier.
 constexpr int kLdsPoses = 6144;
+constexpr int kMaxOffBlocks = 2048;
 
 template <bool IN_LDS>
 __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
-    double* __restrict__ g_poses, int32_t N, const int32_t* __restrict__ ea,
-    const int32_t* __restrict__ eb, const double* __restrict__ tf, int32_t E,
-    const double* __restrict__ invM, const double* __restrict__ gamma, double lr, double sigma) {
-    constexpr int WAVES = kRelaxBlock / 64;
+    double* __restrict__ g_poses, int32_t N, const int32_t* __restrict__ A, const int32_t* __restrict__ B,
+    const double* __restrict__ TF, const int32_t* __restrict__ Kp, const double* __restrict__ C,
+    const double* __restrict__ gamma, double lr, double sigma, int32_t sh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* scan_red = reinterpret_cast<double*>(smem);           // WAVES * 3
-    double* P = IN_LDS ? scan_red + WAVES * 4 : g_poses;
+    const int nblk = ((N - 1) >> sh) + 1;
+    double* off = reinterpret_cast<double*>(smem);                // [nblk][3] lazy offsets
+    double* cA = off + 3 * nblk;                                  // [nblk][3] lazy ramp coefficients
+    double* P = IN_LDS ? cA + 3 * nblk : g_poses;
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int K = *Kp;
+    const int bs = 1 << sh;
 
+    for (int i = tid; i < 3 * nblk; i += kRelaxBlock) {
+        off[i] = 0.0;
+        cA[i] = 0.0;
+    }
     if (IN_LDS) {
         for (int i = tid; i < 3 * N; i += kRelaxBlock) P[i] = g_poses[i];
     }
@@ -214,97 +326,119 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
     }
     const M3 S = diag3(sigma);
 
-    for (int e = 0; e < E; ++e) {
-        const int a = ea[e], b = eb[e];
-        if (!is_loop_edge(a, b) || a >= b) continue;   // a >= b: the reference's no-op
+    // explicit node of thread tid for edge (a, b): the remainder of a's block,
+    // then b's block (when different); -1 when the thread has none
+    auto explicit_node = [&](int a, int b) {
+        const int ba = a >> sh, bb = b >> sh;
+        const int n1 = min(N, (ba + 1) << sh) - (a + 1);
+        const int n2 = bb > ba ? min(N, (bb + 1) << sh) - (bb << sh) : 0;
+        return tid < n1 ? a + 1 + tid : (tid < n1 + n2 ? (bb << sh) + (tid - n1) : -1);
+    };
+    // Edge k's pose-independent operands are loaded during edge k-1.
+    struct Pre {
+        int a, b, ni;
+        double z[9], ca[3], cb[3], ci[3];
+    };
+    auto fetch = [&](int k, Pre& q) {
+        q.a = A[k];
+        q.b = B[k];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) q.z[t] = TF[9 * static_cast<int64_t>(k) + t];
+        q.ni = explicit_node(q.a, q.b);
+        const int i0 = q.ni >= 0 ? q.ni : q.a;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            q.ca[j] = C[3 * (q.a + 1) + j];
+            q.cb[j] = C[3 * (q.b + 1) + j];
+            q.ci[j] = C[3 * (i0 + 1) + j];
+        }
+    };
+    Pre cur, nxt;
+    if (K > 0) fetch(0, cur);
+    for (int k = 0; k < K; ++k) {
+        if (k + 1 < K) fetch(k + 1, nxt);
+        const int a = cur.a, b = cur.b;
 
         // ---- residual (src/pose_graph_optimization.py:29-34), uniform -----------
-        const double pax = P[3 * a], pay = P[3 * a + 1], pat = P[3 * a + 2];
-        const double pbx = P[3 * b], pby = P[3 * b + 1], pbt = P[3 * b + 2];
-        const M3 R = rot_z(pat);                  // construct_R(pg, a)
+        const int ba = a >> sh, bb = b >> sh;
+        double pa[3], pb[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            pa[j] = P[3 * a + j] + off[3 * ba + j] + cA[3 * ba + j] * cur.ca[j];
+            pb[j] = P[3 * b + j] + off[3 * bb + j] + cA[3 * bb + j] * cur.cb[j];
+        }
+        const M3 R = rot_z(pa[2]);                // construct_R(pg, a)
         M3 Pa = R;                                // utils.pose_to_mat(poses[a])
-        Pa.a[0][2] = pax;
-        Pa.a[1][2] = pay;
+        Pa.a[0][2] = pa[0];
+        Pa.a[1][2] = pa[1];
         M3 Z;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) Z.a[k / 3][k % 3] = tf[9 * static_cast<int64_t>(e) + k];
+        for (int t = 0; t < 9; ++t) Z.a[t / 3][t % 3] = cur.z[t];
         const M3 Pb = m3_mul(Pa, Z);
         double r[3];
-        r[0] = Pb.a[0][2] - pbx;
-        r[1] = Pb.a[1][2] - pby;
-        r[2] = py_mod(atan2(Pb.a[1][0], Pb.a[0][0]) - pbt, TWO_PI);
+        r[0] = Pb.a[0][2] - pb[0];
+        r[1] = Pb.a[1][2] - pb[1];
+        r[2] = py_mod(atan2(Pb.a[1][0], Pb.a[0][0]) - pb[2], TWO_PI);
         const M3 Wi = m3_inv(m3_mul(m3_mul(m3_transpose(R), S), R));
-        double d[3];
+        double beta[3], rtw[3];
+        const int L = b - a;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const M3& w = Wi;
-            d[j] = fma(2.0 * w.a[j][2], r[2], fma(2.0 * w.a[j][1], r[1], (2.0 * w.a[j][0]) * r[0]));
-        }
-
-        // ---- prefix of 1/M over (a, b]: chunked block scan (3 columns) ------------
-        const int L = b - a;
-        const int chunk = (L + kRelaxBlock - 1) / kRelaxBlock;
-        const int lo = a + 1 + tid * chunk;
-        const int hi = min(lo + chunk, b + 1);
-        double loc[3] = {0.0, 0.0, 0.0};
-        for (int i = lo; i < hi; ++i) {
-            loc[0] += invM[3 * i + 0];
-            loc[1] += invM[3 * i + 1];
-            loc[2] += invM[3 * i + 2];
-        }
-        // inclusive wave scan of thread totals (Hillis-Steele, fixed order)
-        double inc[3] = {loc[0], loc[1], loc[2]};
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const double o = __shfl_up(inc[j], off, 64);
-                if (lane >= off) inc[j] = o + inc[j];
-            }
-        }
-        if (lane == 63) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) scan_red[wave * 4 + j] = inc[j];
-        }
-        __syncthreads();
-        double pre[3], tw[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double w0 = 0.0, tot = 0.0;
-            for (int w = 0; w < WAVES; ++w) {
-                const double x = scan_red[w * 4 + j];
-                if (w < wave) w0 += x;
-                tot += x;
-            }
-            pre[j] = w0 + (inc[j] - loc[j]);   // exclusive prefix of this thread
-            tw[j] = tot;                        // total_weight
-        }
-        double beta[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double bj = (static_cast<double>(L) * d[j]) * alpha[j];
+            const double dj = fma(2.0 * w.a[j][2], r[2], fma(2.0 * w.a[j][1], r[1], (2.0 * w.a[j][0]) * r[0]));
+            double bj = (static_cast<double>(L) * dj) * alpha[j];
             if (fabs(bj) > fabs(r[j])) bj = r[j];
             beta[j] = bj;
+            rtw[j] = cur.cb[j] - cur.ca[j];           // total_weight over (a, b]
         }
-        // ---- apply: i in (a, b] ramps, i > b shifts by the full beta -------------
+        // ---- explicit nodes (a's block remainder, b's block) ----------------------
         {
-            double run[3] = {pre[0], pre[1], pre[2]};
-            for (int i = lo; i < hi; ++i) {
+            int i = cur.ni;
+            int t = tid;
+            double cij[3] = {cur.ci[0], cur.ci[1], cur.ci[2]};
+            while (i >= 0) {
+                if (i <= b) {
 #pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    run[j] += invM[3 * i + j];
-                    P[3 * i + j] += beta[j] * (run[j] / tw[j]);
+                    for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) / rtw[j]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
                 }
+                t += kRelaxBlock;   // more than one explicit node per thread only when 2^(sh+1) > block
+                if (t >= 2 * bs) break;
+                const int n1 = min(N, (ba + 1) << sh) - (a + 1);
+                const int n2 = bb > ba ? min(N, (bb + 1) << sh) - (bb << sh) : 0;
+                i = t < n1 ? a + 1 + t : (t < n1 + n2 ? (bb << sh) + (t - n1) : -1);
+                if (i >= 0)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) cij[j] = C[3 * (i + 1) + j];
             }
         }
-        for (int i = b + 1 + tid; i < N; i += kRelaxBlock) {
+        // ---- whole blocks: ramp (ba, bb) as C coefficients, tail (bb, nblk) --------
+        for (int q = ba + 1 + tid; q < nblk; q += kRelaxBlock) {
+            if (q < bb) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
+                for (int j = 0; j < 3; ++j) {
+                    const double g = beta[j] / rtw[j];
+                    cA[3 * q + j] += g;
+                    off[3 * q + j] -= g * cur.ca[j];
+                }
+            } else if (q > bb) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) off[3 * q + j] += beta[j];
+            }
         }
         __syncthreads();
+        cur = nxt;
     }
-    if (IN_LDS) {
-        for (int i = tid; i < 3 * N; i += kRelaxBlock) g_poses[i] = P[i];
+    // fold the lazy terms back
+    for (int i = tid; i < N; i += kRelaxBlock) {
+        const int q = i >> sh;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double v = P[3 * i + j] + off[3 * q + j] + cA[3 * q + j] * C[3 * (i + 1) + j];
+            if (IN_LDS) g_poses[3 * i + j] = v; else P[3 * i + j] = v;
+        }
     }
 }
 
@@ -347,7 +481,9 @@ using namespace slamhip;
 extern "C" {
 
 int64_t slam_pgo_sgd_work_size(int32_t N, int32_t E) {
-    return 3 * static_cast<int64_t>(N) + 3 * static_cast<int64_t>(E) + 4;
+    // invM (3N) | dw (3E) | gamma (4) | C (3N+3) | TF (9E) | A, B (E int32 each) | K
+    return 3 * static_cast<int64_t>(N) + 3 * static_cast<int64_t>(E) + 4 + 3 * (static_cast<int64_t>(N) + 1) +
+           9 * static_cast<int64_t>(E) + static_cast<int64_t>(E) + 1;
 }
 
 int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb,
@@ -360,21 +496,31 @@ int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int
     double* invM = work;
     double* dw = work + 3 * static_cast<int64_t>(N);
     double* gamma = dw + 3 * static_cast<int64_t>(E);
+    double* C = gamma + 4;
+    double* TF = C + 3 * (static_cast<int64_t>(N) + 1);
+    int32_t* A = reinterpret_cast<int32_t*>(TF + 9 * static_cast<int64_t>(E));
+    int32_t* Bv = A + E;
+    int32_t* Kp = Bv + E;
     hipLaunchKernelGGL(sgd_dw_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, E,
                        loop_closure_uncertainty, dw);
     hipLaunchKernelGGL(sgd_gamma_kernel, dim3(1), dim3(64), 0, s, ea, eb, E, dw, gamma);
     hipLaunchKernelGGL(sgd_weights_kernel, dim3((N + 127) / 128), dim3(128), 0, s, N, ea, eb, E, dw,
                        invM);
-    const size_t red = 4 * (kRelaxBlock / 64) * sizeof(double);
+    hipLaunchKernelGGL(sgd_prefix_kernel, dim3(1), dim3(kRelaxBlock), 0, s, invM, N, C);
+    hipLaunchKernelGGL(sgd_compact_kernel, dim3(1), dim3(1024), 0, s, ea, eb, tf, E, A, Bv, TF, Kp);
+    // lazy-offset block size 2^sh: >= 64 nodes, at most kMaxOffBlocks blocks
+    int sh = 6;
+    while ((((N - 1) >> sh) + 1) > kMaxOffBlocks) ++sh;
+    const size_t offb = 2 * 3 * static_cast<size_t>(((N - 1) >> sh) + 1) * sizeof(double);   // off + cA
     if (N <= kLdsPoses) {
-        const size_t lds = red + 3 * static_cast<size_t>(N) * sizeof(double);
+        const size_t lds = offb + 3 * static_cast<size_t>(N) * sizeof(double);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxBlock), lds, s, poses, N, ea, eb, tf,
-                           E, invM, gamma, learning_rate, loop_closure_uncertainty);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxBlock), lds, s, poses, N, A, Bv, TF,
+                           Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
     } else {
-        hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxBlock), red, s, poses, N, ea,
-                           eb, tf, E, invM, gamma, learning_rate, loop_closure_uncertainty);
+        hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxBlock), offb, s, poses, N, A, Bv,
+                           TF, Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
     }
     return check_launch("pgo sgd kernels");
 }

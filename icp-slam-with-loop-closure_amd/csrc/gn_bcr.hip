@@ -1,0 +1,517 @@
+// gn_bcr.hip — parallel solve of the Gauss-Newton normal equations by block
+// cyclic reduction (BCR) for gfx950 (MI355X).
+//
+// H is the lower band of half-bandwidth W written by gn_assemble_kernel (nodes
+// in reverse Cuthill-McKee order).  Cut into blocks of Wb >= W rows it is block
+// TRIDIAGONAL: D_i = H[i,i], E_i = H[i+1,i] (every other block is zero).  Level
+// by level (stride s = 1, 2, 4, ...) the "odd" blocks i = s, 3s, 5s, ... are
+// eliminated in parallel — one workgroup each — and their Schur complements
+// update the "even" neighbours:
+//   C_i C_i^T = D_i,  X_i = C_i^-1 E_p,  Y_i = C_i^-1 E_i^T,  z_i = C_i^-1 b_i
+//   D_p -= X_i^T X_i,  D_n -= Y_i^T Y_i,  E'_p = -Y_i^T X_i,
+//   b_p -= X_i^T z_i,  b_n -= Y_i^T z_i                      (p = i - s, n = i + s)
+// until only block 0 remains; back-substitution walks the levels in reverse:
+//   x_i = C_i^-T (z_i - X_i x_p - Y_i x_n).
+// log2(nv / Wb) dependent levels of dense Wb x Wb work instead of nv / 16
+// dependent band steps (C4: 8 levels vs 938 steps).  The elimination order
+// differs from the band Cholesky, so results agree to rounding (tests: 1e-8
+// against oracle/gn_oracle.py).  Used when Wb <= kBcrMaxWb and nv / Wb >= 4.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace slamhip {
+
+constexpr int kBcrThreads = 256;
+constexpr int kBcrMaxWb = 96;
+
+__host__ __device__ inline int64_t bcr_blk(int Wb) { return static_cast<int64_t>(Wb) * Wb; }
+
+// Band (row r holds (r, r-d), d = 0..W) -> D_i (full symmetric), E_i, b_i;
+// rows past nv are padded with the identity.
+__global__ void bcr_load_kernel(const double* __restrict__ Hb, const double* __restrict__ rhs, int32_t nv,
+                                int32_t W, int32_t Wb, int32_t nb, double* __restrict__ D, double* __restrict__ E,
+                                double* __restrict__ bz) {
+    const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (idx >= nb * bcr_blk(Wb)) return;
+    const int i = static_cast<int>(idx / bcr_blk(Wb));
+    const int r = static_cast<int>((idx / Wb) % Wb), c = static_cast<int>(idx % Wb);
+    const int64_t ld = W + 1;
+    const int R = i * Wb + r, Cc = i * Wb + c;
+    const int lo = max(R, Cc), d = abs(R - Cc);
+    double v = 0.0;
+    if (lo < nv) {
+        if (d <= W) v = Hb[lo * ld + d];
+    } else if (R == Cc) {
+        v = 1.0;
+    }
+    D[idx] = v;
+    if (i + 1 < nb) {
+        const int R2 = R + Wb, d2 = R2 - Cc;
+        E[idx] = (R2 < nv && d2 <= W) ? Hb[R2 * ld + d2] : 0.0;
+    }
+    if (c == 0) bz[static_cast<int64_t>(i) * Wb + r] = R < nv ? rhs[R] : 0.0;
+}
+
+// ---- blocked dense kernels on a Wb x Wb LDS tile (Wb a multiple of 16) -------
+// Every loop below has compile-time trip counts inside a 16-wide block, so the
+// LDS reads of a block issue back to back instead of one latency per FMA.
+
+// Wave 0, lanes 0..15: factor the 16 x 16 diagonal block at k0 in registers
+// (lane i holds row i; pivots and L[c][j] broadcast with v_readlane).
+__device__ inline bool bcr_diag16(double* Cm, int ldc, int k0) {
+    const int lane = threadIdx.x & 63;
+    double row[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) row[c] = (lane < 16 && c <= lane) ? Cm[(k0 + lane) * ldc + k0 + c] : 0.0;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const double piv = readlane_d(row[j], j);
+        bad |= !(piv > 0.0);
+        const double d = sqrt(piv);
+        if (lane == j) row[j] = d;
+        if (lane > j) row[j] = row[j] / d;
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) {
+            const double lcj = readlane_d(row[j], c);
+            if (lane >= c) row[c] = fma(-row[j], lcj, row[c]);
+        }
+    }
+    if (lane < 16)
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            if (c <= lane) Cm[(k0 + lane) * ldc + k0 + c] = row[c];
+    return bad;
+}
+
+// Blocked right-looking Cholesky of the LDS tile (lower triangle), all
+// threads; returns through *status on a non-positive pivot.
+__device__ inline void bcr_chol(double* Cm, int ldc, int Wb, int32_t* status) {
+    const int tid = threadIdx.x;
+    for (int k0 = 0; k0 < Wb; k0 += 16) {
+        if (tid < 64) {
+            const bool bad = bcr_diag16(Cm, ldc, k0);
+            if (bad && tid == 0 && status) *status = 1;
+        }
+        __syncthreads();
+        const int r0 = k0 + 16, n = Wb - r0;
+        // panel: L[r][k0+t] = (A[r][k0+t] - sum_q L[r][k0+q] L[k0+t][k0+q]) / L[k0+t][k0+t]
+        for (int i = tid; i < n; i += kBcrThreads) {
+            asm volatile("" ::: "memory");   // keep the L_KK reads in the loop (no hoisting into 272 VGPRs)
+            const int r = r0 + i;
+            double l[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                asm volatile("" ::: "memory");
+                double v = Cm[r * ldc + k0 + t];
+#pragma unroll
+                for (int q = 0; q < t; ++q) v = fma(-l[q], Cm[(k0 + t) * ldc + k0 + q], v);
+                l[t] = v / Cm[(k0 + t) * ldc + k0 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t) Cm[r * ldc + k0 + t] = l[t];
+        }
+        __syncthreads();
+        // trailing update of the lower triangle, 4 x 4 register tiles
+        const int nt = n >> 2;
+        for (int q = tid; q < nt * (nt + 1) / 2; q += kBcrThreads) {
+            asm volatile("" ::: "memory");
+            int ti = static_cast<int>((sqrtf(8.0f * q + 1.0f) - 1.0f) * 0.5f);
+            while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+            while (ti * (ti + 1) / 2 > q) --ti;
+            const int tj = q - ti * (ti + 1) / 2;
+            double acc[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
+#pragma unroll 4
+            for (int t = 0; t < 16; ++t) {
+                double a[4], b[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a[u] = Cm[(r0 + 4 * ti + u) * ldc + k0 + t];
+                    b[u] = Cm[(r0 + 4 * tj + u) * ldc + k0 + t];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int r = r0 + 4 * ti + u, c = r0 + 4 * tj + v;
+                    if (c <= r) Cm[r * ldc + c] -= acc[u][v];
+                }
+        }
+        __syncthreads();
+    }
+}
+
+// Blocked forward substitution C X = R in place for nc columns of R (LDS,
+// row stride ldr), all threads.
+__device__ inline void bcr_trsm(const double* Cm, int ldc, double* Rm, int ldr, int Wb, int nc) {
+    const int tid = threadIdx.x;
+    for (int k0 = 0; k0 < Wb; k0 += 16) {
+        // diagonal block: one thread per column
+        for (int c = tid; c < nc; c += kBcrThreads) {
+            asm volatile("" ::: "memory");   // keep the L_KK reads in the loop
+            double x[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                asm volatile("" ::: "memory");   // row t's reads stay in step t (bounded live registers)
+                double v = Rm[(k0 + t) * ldr + c];
+#pragma unroll
+                for (int q = 0; q < t; ++q) v = fma(-Cm[(k0 + t) * ldc + k0 + q], x[q], v);
+                x[t] = v / Cm[(k0 + t) * ldc + k0 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t) Rm[(k0 + t) * ldr + c] = x[t];
+        }
+        __syncthreads();
+        // rows below: R[r][c] -= sum_t L[r][k0+t] X[k0+t][c], 4 x 4 tiles
+        const int r0 = k0 + 16, nr = (Wb - r0) >> 2, ncl = (nc + 3) >> 2;
+        for (int q = tid; q < nr * ncl; q += kBcrThreads) {
+            asm volatile("" ::: "memory");
+            const int ti = q / ncl, tj = q % ncl;
+            double acc[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
+#pragma unroll 4
+            for (int t = 0; t < 16; ++t) {
+                double a[4], b[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a[u] = Cm[(r0 + 4 * ti + u) * ldc + k0 + t];
+                    const int c = 4 * tj + u;
+                    b[u] = c < nc ? Rm[(k0 + t) * ldr + c] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int c = 4 * tj + v;
+                    if (c < nc) Rm[(r0 + 4 * ti + u) * ldr + c] -= acc[u][v];
+                }
+        }
+        __syncthreads();
+    }
+}
+
+// Odd blocks of level s, two workgroups per block (blockIdx.y): both factor
+// C_i (cheap next to the solves); part 0 solves X = C^-1 E_p, part 1 solves
+// [Y | z] = C^-1 [E_i^T | b_i] and stores C_i (into Cs, never over D: the
+// other part may still be reading D_i).
+__global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __restrict__ D,
+                                                              const double* __restrict__ E, double* __restrict__ Cs,
+                                                              double* __restrict__ Xs, double* __restrict__ Ys,
+                                                              double* __restrict__ bz, int32_t Wb, int32_t nb,
+                                                              int32_t s, int32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int ldc = Wb + 1, ldr = Wb + 2;
+    double* Cm = lds;                                   // [Wb][Wb + 1]
+    double* Rm = lds + static_cast<int64_t>(Wb) * ldc;  // [Wb][Wb + 2]
+    const int tid = threadIdx.x;
+    const int part = blockIdx.y;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const int64_t B2 = bcr_blk(Wb);
+    const double* Di = D + i * B2;
+    const double* Ep = E + p * B2;                      // A[i, p]: rows of i, columns of p
+    const double* Ei = E + i * B2;                      // A[n, i]; A[i, n] = its transpose
+    for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+        const int r = e / Wb, c = e % Wb;
+        Cm[r * ldc + c] = Di[e];
+        if (part == 0) Rm[r * ldr + c] = Ep[e];
+        else Rm[r * ldr + c] = n < nb ? Ei[c * Wb + r] : 0.0;
+    }
+    if (part == 1)
+        for (int r = tid; r < Wb; r += kBcrThreads) Rm[r * ldr + Wb] = bz[static_cast<int64_t>(i) * Wb + r];
+    __syncthreads();
+    bcr_chol(Cm, ldc, Wb, part == 1 ? status : nullptr);
+    bcr_trsm(Cm, ldc, Rm, ldr, Wb, part == 0 ? Wb : Wb + 1);
+    if (part == 0) {
+        double* Xi = Xs + i * B2;
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) Xi[e] = Rm[(e / Wb) * ldr + e % Wb];
+    } else {
+        double* Yi = Ys + i * B2;
+        double* Ci = Cs + i * B2;
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+            const int r = e / Wb, c = e % Wb;
+            Yi[e] = Rm[r * ldr + c];
+            Ci[e] = c <= r ? Cm[r * ldc + c] : 0.0;
+        }
+        for (int r = tid; r < Wb; r += kBcrThreads) bz[static_cast<int64_t>(i) * Wb + r] = Rm[r * ldr + Wb];
+    }
+}
+
+// Even blocks of level s: Schur updates from the odd neighbours i1 = j - s
+// (its n is j) and i2 = j + s (its p is j), and the new coupling to j + 2s.
+// 16 x 16 threads, each a (Wb/16) x (Wb/16) register tile; the factors are
+// staged in LDS (A^T B products read columns k of both).
+template <int T>   // T = Wb / 16: register tile edge
+__global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restrict__ D, double* __restrict__ E,
+                                                               const double* __restrict__ Xs,
+                                                               const double* __restrict__ Ys,
+                                                               double* __restrict__ bz, int32_t Wb, int32_t nb,
+                                                               int32_t s) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int ld = Wb + 1;
+    double* L1 = lds;                                   // [Wb][Wb + 1]
+    double* L2 = lds + static_cast<int64_t>(Wb) * ld;   // [Wb][Wb + 1]
+    double* zv = L2 + static_cast<int64_t>(Wb) * ld;    // [2][Wb]
+    const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+    constexpr int nt = T;
+    const int j = 2 * s * blockIdx.x;
+    const int i1 = j - s, i2 = j + s;
+    // part 0 (blockIdx.y): D_j and b_j updates; part 1: the new coupling E'_j
+    const int part = blockIdx.y;
+    const bool hE = part == 1 && i2 < nb && j + 2 * s < nb;
+    const bool h1 = part == 0 && i1 >= 0, h2 = (part == 0 && i2 < nb) || hE;
+    if (!h1 && !h2) return;
+    const int64_t B2 = bcr_blk(Wb);
+    double acc[T][T], accE[T][T];
+#pragma unroll
+    for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int v = 0; v < T; ++v) {
+            acc[u][v] = 0.0;
+            accE[u][v] = 0.0;
+        }
+    double bacc = 0.0;   // thread tid < Wb: row tid of the rhs update
+    if (h1) {   // D_j -= Y1^T Y1, b_j -= Y1^T z1
+        const double* Y1 = Ys + i1 * B2;
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) L1[(e / Wb) * ld + e % Wb] = Y1[e];
+        for (int r = tid; r < Wb; r += kBcrThreads) zv[r] = bz[static_cast<int64_t>(i1) * Wb + r];
+        __syncthreads();
+        for (int k = 0; k < Wb; ++k) {
+            double a[T], b[T];
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                a[u] = u < nt ? L1[k * ld + tr + 16 * u] : 0.0;
+                b[u] = u < nt ? L1[k * ld + tc + 16 * u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < T; ++u)
+#pragma unroll
+                for (int v = 0; v < T; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+        }
+        if (tid < Wb)
+            for (int k = 0; k < Wb; ++k) bacc = fma(L1[k * ld + tid], zv[k], bacc);
+        __syncthreads();
+    }
+    if (h2) {   // D_j -= X2^T X2, b_j -= X2^T z2, E'_j = -Y2^T X2
+        const double* X2 = Xs + i2 * B2;
+        const double* Y2 = Ys + i2 * B2;
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+            L1[(e / Wb) * ld + e % Wb] = X2[e];
+            if (hE) L2[(e / Wb) * ld + e % Wb] = Y2[e];
+        }
+        // part 1 only needs Y2^T X2; part 0 only X2^T X2
+        for (int r = tid; r < Wb; r += kBcrThreads) zv[Wb + r] = bz[static_cast<int64_t>(i2) * Wb + r];
+        __syncthreads();
+        for (int k = 0; k < Wb; ++k) {
+            double a[T], b[T], y[T];
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                a[u] = u < nt ? L1[k * ld + tr + 16 * u] : 0.0;
+                b[u] = u < nt ? L1[k * ld + tc + 16 * u] : 0.0;
+                y[u] = (hE && u < nt) ? L2[k * ld + tr + 16 * u] : 0.0;
+            }
+            if (hE) {
+#pragma unroll
+                for (int u = 0; u < T; ++u)
+#pragma unroll
+                    for (int v = 0; v < T; ++v) accE[u][v] = fma(y[u], b[v], accE[u][v]);
+            } else {
+#pragma unroll
+                for (int u = 0; u < T; ++u)
+#pragma unroll
+                    for (int v = 0; v < T; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+            }
+        }
+        if (!hE && tid < Wb)
+            for (int k = 0; k < Wb; ++k) bacc = fma(L1[k * ld + tid], zv[Wb + k], bacc);
+    }
+    double* Dj = D + j * B2;
+    double* Ej = E + j * B2;
+#pragma unroll
+    for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int v = 0; v < T; ++v) {
+            if (u < nt && v < nt) {
+                const int r = tr + 16 * u, c = tc + 16 * v;
+                if (hE) Ej[r * Wb + c] = -accE[u][v];
+                else Dj[r * Wb + c] -= acc[u][v];
+            }
+        }
+    if (part == 0 && tid < Wb) bz[static_cast<int64_t>(j) * Wb + tid] -= bacc;
+}
+
+// Backward substitution C^T x = v by one wave, C lower in LDS (stride ldc);
+// v in lanes (rows lane, lane + 64); returns x in the same layout.
+__device__ inline void bcr_backsub_wave(const double* Cm, int ldc, int Wb, double& v0, double& v1) {
+    const int lane = threadIdx.x & 63;
+    for (int k = Wb - 1; k >= 0; --k) {
+        const double vk = k < 64 ? readlane_d(v0, k) : readlane_d(v1, k - 64);
+        const double xk = vk / Cm[k * ldc + k];
+        if (lane == k) v0 = xk;
+        if (lane + 64 == k) v1 = xk;
+        if (lane < k) v0 = fma(-Cm[k * ldc + lane], xk, v0);
+        if (lane + 64 < k) v1 = fma(-Cm[k * ldc + lane + 64], xk, v1);
+    }
+}
+
+// Last block (index 0): Cholesky and both substitutions -> x_0.
+__global__ __launch_bounds__(kBcrThreads) void bcr_top_kernel(double* __restrict__ D, const double* __restrict__ bz,
+                                                              double* __restrict__ x, int32_t Wb,
+                                                              int32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int ldc = Wb + 1;
+    double* Cm = lds;
+    double* y = lds + static_cast<int64_t>(Wb) * ldc;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < Wb * Wb; e += kBcrThreads) Cm[(e / Wb) * ldc + e % Wb] = D[e];
+    for (int r = tid; r < Wb; r += kBcrThreads) y[r] = bz[r];
+    __syncthreads();
+    bcr_chol(Cm, ldc, Wb, status);
+    bcr_trsm(Cm, ldc, y, 1, Wb, 1);
+    if (tid < 64) {
+        double v0 = tid < Wb ? y[tid] : 0.0, v1 = tid + 64 < Wb ? y[tid + 64] : 0.0;
+        bcr_backsub_wave(Cm, ldc, Wb, v0, v1);
+        if (tid < Wb) x[tid] = v0;
+        if (tid + 64 < Wb) x[tid + 64] = v1;
+    }
+}
+
+// Back-substitution of the odd blocks of level s: v = z - X x_p - Y x_n with
+// two threads per row (halves of k, x_p / x_n staged in LDS), then C^-T v by
+// one wave.
+__global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __restrict__ Cs,
+                                                               const double* __restrict__ Xs,
+                                                               const double* __restrict__ Ys,
+                                                               const double* __restrict__ bz, double* __restrict__ x,
+                                                               int32_t Wb, int32_t nb, int32_t s) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int ldc = Wb + 1;
+    double* Cm = lds;
+    double* vv = lds + static_cast<int64_t>(Wb) * ldc;     // [Wb]
+    double* xpn = vv + Wb;                                  // [2][Wb]
+    const int tid = threadIdx.x;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const int64_t B2 = bcr_blk(Wb);
+    const double* Ci = Cs + i * B2;
+    for (int e = tid; e < Wb * Wb; e += kBcrThreads) Cm[(e / Wb) * ldc + e % Wb] = Ci[e];
+    for (int k = tid; k < Wb; k += kBcrThreads) {
+        xpn[k] = x[static_cast<int64_t>(p) * Wb + k];
+        xpn[Wb + k] = n < nb ? x[static_cast<int64_t>(n) * Wb + k] : 0.0;
+    }
+    __syncthreads();
+    {
+        const int r = tid >> 1, h = tid & 1;
+        double v = 0.0;
+        if (r < Wb) {
+            const double* X = Xs + i * B2 + static_cast<int64_t>(r) * Wb;
+            const double* Y = Ys + i * B2 + static_cast<int64_t>(r) * Wb;
+            const int k0 = h * (Wb >> 1), k1 = k0 + (Wb >> 1);
+            double v1 = 0.0;
+#pragma unroll 8
+            for (int k = k0; k < k1; ++k) {
+                v = fma(X[k], xpn[k], v);
+                v1 = fma(Y[k], xpn[Wb + k], v1);
+            }
+            v += v1;
+        }
+        v += __shfl_xor(v, 1, 64);
+        if (r < Wb && h == 0) vv[r] = bz[static_cast<int64_t>(i) * Wb + r] - v;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        double v0 = tid < Wb ? vv[tid] : 0.0, v1 = tid + 64 < Wb ? vv[tid + 64] : 0.0;
+        bcr_backsub_wave(Cm, ldc, Wb, v0, v1);
+        double* xi = x + static_cast<int64_t>(i) * Wb;
+        if (tid < Wb) xi[tid] = v0;
+        if (tid + 64 < Wb) xi[tid + 64] = v1;
+    }
+}
+
+// ---- host ------------------------------------------------------------------
+
+int bcr_block_rows(int32_t nv, int32_t W) {
+    const int Wb = ((max(W, 1) + 15) / 16) * 16;
+    if (Wb > kBcrMaxWb) return 0;
+    if ((nv + Wb - 1) / Wb < 4) return 0;
+    return Wb;
+}
+
+int64_t bcr_work_size(int32_t nv, int32_t W) {
+    const int Wb = ((max(W, 1) + 15) / 16) * 16;
+    const int64_t nb = (nv + Wb - 1) / Wb;
+    return 5 * nb * bcr_blk(Wb) + 2 * nb * Wb;
+}
+
+// Solve H dx = rhs (H in band storage, work of bcr_work_size doubles); *dx_out
+// points at the solution inside `work` (first nv entries).
+int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
+              double** dx_out, int32_t* status, hipStream_t st) {
+    const int nb = (nv + Wb - 1) / Wb;
+    const int64_t B2 = bcr_blk(Wb);
+    double* D = work;
+    double* E = D + nb * B2;
+    double* Xs = E + nb * B2;
+    double* Ys = Xs + nb * B2;
+    double* Cs = Ys + nb * B2;
+    double* bz = Cs + nb * B2;
+    double* dx = bz + static_cast<int64_t>(nb) * Wb;
+    *dx_out = dx;
+    const int64_t tot = nb * B2;
+    hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs, nv,
+                       W, Wb, nb, D, E, bz);
+    const size_t lds_odd = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + static_cast<size_t>(Wb) * (Wb + 2));
+    const size_t lds_even = sizeof(double) * (2 * static_cast<size_t>(Wb) * (Wb + 1) + 2 * static_cast<size_t>(Wb));
+    const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 3 * static_cast<size_t>(Wb));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bcr_odd_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_odd));
+    using EvenFn = void (*)(double*, double*, const double*, const double*, double*, int32_t, int32_t, int32_t);
+    static const EvenFn evens[6] = {bcr_even_kernel<1>, bcr_even_kernel<2>, bcr_even_kernel<3>,
+                                    bcr_even_kernel<4>, bcr_even_kernel<5>, bcr_even_kernel<6>};
+    const EvenFn even = evens[Wb / 16 - 1];
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(even), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds_even));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bcr_back_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_back));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bcr_top_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_back));
+    int s = 1;
+    for (; s < nb; s *= 2) {
+        const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
+        const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
+        hipLaunchKernelGGL(bcr_odd_kernel, dim3(n_odd, 2), dim3(kBcrThreads), lds_odd, st, D, E, Cs, Xs, Ys, bz, Wb,
+                           nb, s, status);
+        hipLaunchKernelGGL(even, dim3(n_even, 2), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
+    }
+    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
+    for (s /= 2; s >= 1; s /= 2) {
+        const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
+        hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(kBcrThreads), lds_back, st, Cs, Xs, Ys, bz, dx, Wb,
+                           nb, s);
+    }
+    return check_launch("gn bcr kernels");
+}
+
+}  // namespace slamhip

@@ -476,21 +476,35 @@ __global__ void gn_update_kernel(double* __restrict__ poses, int32_t N, const in
     poses[3 * n + 2] = wrap_pi(poses[3 * n + 2] + dx[c + 2]);
 }
 
-// chi2 = sum_e w_e |e_e|^2, deterministic single-block reduction.
-__global__ __launch_bounds__(256) void gn_chi2_kernel(const double* __restrict__ contrib, int32_t E,
-                                                      double* __restrict__ out) {
-    __shared__ double red[4];
-    double v[1] = {0.0};
-    for (int e = threadIdx.x; e < E; e += 256) v[0] += contrib[static_cast<int64_t>(e) * kGnContrib + 33];
-    block_sum<1, 4>(v, red);
+// chi2 = sum_e w_e |e_e|^2, deterministic single-block reduction (1024
+// threads, four independent partial sums per thread).
+__global__ __launch_bounds__(1024) void gn_chi2_kernel(const double* __restrict__ contrib, int32_t E,
+                                                       double* __restrict__ out) {
+    __shared__ double red[16];
+    double q[4] = {0.0, 0.0, 0.0, 0.0};
+    int e = threadIdx.x;
+    for (; e + 3 * 1024 < E; e += 4 * 1024)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] += contrib[static_cast<int64_t>(e + u * 1024) * kGnContrib + 33];
+    for (; e < E; e += 1024) q[0] += contrib[static_cast<int64_t>(e) * kGnContrib + 33];
+    double v[1] = {(q[0] + q[1]) + (q[2] + q[3])};
+    block_sum<1, 16>(v, red);
     if (threadIdx.x == 0) *out = v[0];
 }
 
 }  // namespace slamhip
 
+namespace slamhip {
+int bcr_block_rows(int32_t nv, int32_t W);
+int64_t bcr_work_size(int32_t nv, int32_t W);
+int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
+              double** dx_out, int32_t* status, hipStream_t st);
+}  // namespace slamhip
+
 using namespace slamhip;
 
 static unsigned long long* g_gn_stamps = nullptr;
+static int g_gn_solver = 0;   // 0 auto, 1 band Cholesky, 2 block cyclic reduction
 
 extern "C" {
 
@@ -498,6 +512,16 @@ extern "C" {
 // per-phase s_memtime totals (NULL disables).
 int slam_gn_set_stamps(void* dev_buf) {
     g_gn_stamps = reinterpret_cast<unsigned long long*>(dev_buf);
+    return ok();
+}
+
+int slam_gn_bcr_block_rows(int32_t nv, int32_t W) { return bcr_block_rows(nv, W); }
+
+// Diagnostics: force the linear solver (0 auto, 1 band Cholesky, 2 block
+// cyclic reduction when the band allows it).
+int slam_gn_set_solver(int mode) {
+    if (mode < 0 || mode > 2) return fail(SLAM_EINVAL, "gn solver %d not in {0, 1, 2}", mode);
+    g_gn_solver = mode;
     return ok();
 }
 
@@ -512,7 +536,8 @@ int64_t slam_gn_work_size(int32_t N, int32_t E, int32_t W) {
     const int64_t MP = window_dim(W);
     const int64_t steps = (nv + kGnS - 1) / kGnS;
     return static_cast<int64_t>(E) * kGnContrib + nv * (W + 1) + nv + MP * (MP + 1) +
-           static_cast<int64_t>(kGnS) * lpw(W) + MP + steps * (kGnS + W) * kGnS + 8;
+           static_cast<int64_t>(kGnS) * lpw(W) + MP + steps * (kGnS + W) * kGnS + 8 +
+           bcr_work_size(static_cast<int32_t>(nv), W);
 }
 
 int slam_gn_max_lds_band(void) {
@@ -541,13 +566,24 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, tf, w, E,
                            contrib);
-    hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(256), 0, s, contrib, E, out_chi2);
+    hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, contrib, E, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
     if (hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nv) * (W + 1), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (n_slots > 0)
         hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128), dim3(128), 0, s, contrib, slot_rc,
                            slot_ptr, slot_items, n_slots, W, Hb, rhs);
+    const int Wb = g_gn_solver == 1 ? 0 : bcr_block_rows(nv, W);
+    if (Wb > 0) {   // block cyclic reduction: log2(nv / Wb) parallel levels
+        const int64_t MPw = window_dim(W);
+        const int64_t steps = (static_cast<int64_t>(nv) + kGnS - 1) / kGnS;
+        double* bwork = gwin + MPw * (MPw + 1) + static_cast<int64_t>(kGnS) * lpw(W) + MPw + steps * (kGnS + W) * kGnS + 8;
+        double* dx = nullptr;
+        const int rc = bcr_solve(Hb, rhs, nv, W, Wb, bwork, &dx, status, s);
+        if (rc != 0) return rc;
+        hipLaunchKernelGGL(gn_update_kernel, dim3((N + 255) / 256), dim3(256), 0, s, poses, N, node_col, dx);
+        return check_launch("gn kernels");
+    }
     int MP = 32;
     while (MP < W + kGnS) MP <<= 1;
     const size_t lds_need = sizeof(double) * (static_cast<size_t>(MP) * (MP + 1) + static_cast<size_t>(kGnS) * lpw(W) + MP);

@@ -41,6 +41,8 @@ SIGNATURES = {
     "slam_gn_work_size": (c_i64, [c_int, c_int, c_int]),
     "slam_gn_max_lds_band": (c_int, []),
     "slam_gn_set_stamps": (c_int, [c_ptr]),
+    "slam_gn_set_solver": (c_int, [c_int]),
+    "slam_gn_bcr_block_rows": (c_int, [c_int, c_int]),
     "slam_gn_iteration_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                       c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr]),
 }
@@ -59,6 +61,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is not built: run `make -C {os.path.dirname(_HERE)}/csrc` "
                               "or __graft_entry__.build()")
+        # Device pointers and streams come from PyTorch's HIP runtime: load it
+        # first, so the library binds to that libamdhip64 instead of pulling in
+        # a second copy (two runtimes in one process -> invalid pointers).
+        import torch  # noqa: F401
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             if not hasattr(handle, name):

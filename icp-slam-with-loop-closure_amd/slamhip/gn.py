@@ -153,4 +153,6 @@ def bench_c4(iterations=10, reps=3):
         best = dt if best is None else min(best, dt)
     return {"gn_iters_per_sec": round(iterations / best, 2), "gn_ms_per_iter": round(best / iterations * 1e3, 4),
             "gn_graph": f"{len(guess)} nodes / {len(ea)} edges (C4)", "gn_band_W": plan.W,
-            "gn_plan_s": round(plan_s, 3), "gn_chi2_first_last": [float(chis[0]), float(chis[-1])]}
+            "gn_plan_s": round(plan_s, 3), "gn_chi2_first_last": [float(chis[0]), float(chis[-1])],
+            "gn_solver": "block cyclic reduction (Wb=%d)" % _abi.lib().slam_gn_bcr_block_rows(plan.nv, plan.W)
+            if _abi.lib().slam_gn_bcr_block_rows(plan.nv, plan.W) > 0 else "band Cholesky"}

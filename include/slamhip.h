@@ -164,6 +164,11 @@ int slam_icp_selected_instance(int max_n1);
  * identical results. */
 int slam_icp_set_screen(int mode);
 int slam_gn_set_stamps(void* dev_buf);
+/* GN linear solver: 0 auto (block cyclic reduction when the band allows it),
+ * 1 band Cholesky, 2 block cyclic reduction (falls back to 1 if not allowed). */
+int slam_gn_set_solver(int mode);
+/* Block rows of the cyclic-reduction solver for (nv, W), 0 = not applicable. */
+int slam_gn_bcr_block_rows(int32_t nv, int32_t W);
 int slam_icp_set_stamps(void* dev_buf);
 /* Count candidate-distance evaluations performed (all lanes) into a device
  * uint64 (atomic add per wave); NULL turns counting off. */

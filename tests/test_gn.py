@@ -74,8 +74,10 @@ def test_oracle_converges_on_c4():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("iters", [1, 3])
-def test_gn_small_vs_oracle(iters):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gn_small_vs_oracle(solver, iters, mode):
     from slamhip import gn
+    solver(mode)
     guess, ea, eb, tf = _random_graph(80, 30, 2)
     ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=iters)
     got, chi = gn.optimize(guess, ea, eb, tf, iterations=iters)
@@ -84,11 +86,28 @@ def test_gn_small_vs_oracle(iters):
     assert np.abs(go.wrap(got[:, 2] - ref[:, 2])).max() <= 1e-8
 
 
+@pytest.fixture
+def solver():
+    """Select the GN linear solver for one test (1 band Cholesky, 2 block cyclic reduction)."""
+    from slamhip import _abi
+    lib = _abi.lib()
+
+    def use(mode):
+        assert lib.slam_gn_set_solver(mode) == 0
+    yield use
+    lib.slam_gn_set_solver(0)
+
+
 @pytest.mark.gpu
-def test_gn_c4_vs_oracle():
-    """Config C4: 5,000 nodes / 20,000 edges, 5 iterations."""
-    from slamhip import gn, synthetic
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gn_c4_vs_oracle(solver, mode):
+    """Config C4: 5,000 nodes / 20,000 edges, 5 iterations, both linear solvers."""
+    from slamhip import _abi, gn, synthetic
+    solver(mode)
     guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
+    if mode == 2:
+        p = gn.GnPlan(len(guess), ea, eb)
+        assert _abi.lib().slam_gn_bcr_block_rows(p.nv, p.W) > 0
     ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=5)
     got, chi = gn.optimize(guess, ea, eb, tf, iterations=5)
     assert np.allclose(chi, ref_chi, rtol=1e-8)
@@ -133,12 +152,14 @@ def test_optimize_pose_graph_dropin():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_nodes", [40, 600])
-def test_gn_narrow_band(n_nodes):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gn_narrow_band(solver, n_nodes, mode):
     """Bands narrower than the 16-column Cholesky block (W < S): pure chains
     (W = 5) and a loop sequence whose RCM order folds the ring (W = 14) — the
     look-ahead must not read panel rows beyond the band."""
     from slamhip import gn, synthetic
     import src.pose_graph as pgm
+    solver(mode)
     s = synthetic.make_loop_sequence(n_nodes, seed=4)
     pg = pgm.PoseGraph(s.odometry.copy())
     for i, j in s.loop_pairs:
@@ -147,5 +168,23 @@ def test_gn_narrow_band(n_nodes):
     assert gn.GnPlan(n_nodes, ea, eb).W < 16
     ref, ref_chi = go.optimize(s.odometry.copy(), ea, eb, tf, iterations=3)
     got, chi = gn.optimize(s.odometry.copy(), ea, eb, tf, iterations=3)
+    assert np.allclose(chi, ref_chi, rtol=1e-8)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(25, 3, 200), (40, 4, 500), (25, 6, 400), (30, 8, 800), (60, 12, 2000)])
+def test_gn_bcr_block_sizes(shape):
+    """Lap graphs whose RCM bands give cyclic-reduction blocks of 32, 48, 64
+    and 96 rows (register tiles 2..6), and one too wide for it (W = 125 ->
+    band Cholesky): both paths against the oracle."""
+    from slamhip import _abi, gn, synthetic
+    pps, nl, nloops = shape
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=pps, num_loops=nl, n_loops=nloops)
+    p = gn.GnPlan(len(guess), ea, eb)
+    Wb = _abi.lib().slam_gn_bcr_block_rows(p.nv, p.W)
+    assert (Wb == 0) == (p.W > 96)
+    ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=3)
+    got, chi = gn.optimize(guess, ea, eb, tf, iterations=3)
     assert np.allclose(chi, ref_chi, rtol=1e-8)
     assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8

@@ -485,18 +485,22 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     const size_t lds_odd = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + static_cast<size_t>(Wb) * (Wb + 2));
     const size_t lds_even = sizeof(double) * (2 * static_cast<size_t>(Wb) * (Wb + 1) + 2 * static_cast<size_t>(Wb));
     const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 3 * static_cast<size_t>(Wb));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bcr_odd_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_odd));
     using EvenFn = void (*)(double*, double*, const double*, const double*, double*, int32_t, int32_t, int32_t);
     static const EvenFn evens[6] = {bcr_even_kernel<1>, bcr_even_kernel<2>, bcr_even_kernel<3>,
                                     bcr_even_kernel<4>, bcr_even_kernel<5>, bcr_even_kernel<6>};
     const EvenFn even = evens[Wb / 16 - 1];
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(even), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds_even));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bcr_back_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_back));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bcr_top_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_back));
+    // dynamic-LDS limits are raised once (not a stream operation: keeps the
+    // launch sequence capturable into a hipGraph)
+    static bool attrs = false;
+    if (!attrs) {
+        const int lim = 160 * 1024;
+        const void* fns[] = {reinterpret_cast<const void*>(bcr_odd_kernel), reinterpret_cast<const void*>(bcr_back_kernel),
+                             reinterpret_cast<const void*>(bcr_top_kernel)};
+        for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+        for (const EvenFn f : evens)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+        attrs = true;
+    }
     int s = 1;
     for (; s < nb; s *= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb

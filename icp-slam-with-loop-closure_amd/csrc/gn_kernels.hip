@@ -589,8 +589,12 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
     const size_t lds_need = sizeof(double) * (static_cast<size_t>(MP) * (MP + 1) + static_cast<size_t>(kGnS) * lpw(W) + MP);
     double* PS = gwin + static_cast<int64_t>(MP) * (MP + 1) + static_cast<int64_t>(kGnS) * lpw(W) + MP;
     if (lds_need + 4096 <= 160 * 1024) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_factor_kernel<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_need));
+        static bool attr_f = false;   // once: keeps the launch sequence graph-capturable
+        if (!attr_f) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_factor_kernel<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+            attr_f = true;
+        }
         hipLaunchKernelGGL(gn_factor_kernel<true>, dim3(1), dim3(kGnFBlock), lds_need, s, Hb, rhs, nv, W, MP, gwin,
                            gwin, PS, status, g_gn_stamps);
     } else {
@@ -599,8 +603,12 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
     }
     const size_t x_bytes = sizeof(double) * static_cast<size_t>(nv);
     if (x_bytes <= 150 * 1024) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_backsolve_kernel<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(x_bytes));
+        static bool attr_b = false;
+        if (!attr_b) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gn_backsolve_kernel<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+            attr_b = true;
+        }
         hipLaunchKernelGGL(gn_backsolve_kernel<true>, dim3(1), dim3(kGnBlock), x_bytes, s, PS, nv, W, rhs);
     } else {
         hipLaunchKernelGGL(gn_backsolve_kernel<false>, dim3(1), dim3(kGnBlock), 0, s, PS, nv, W, rhs);

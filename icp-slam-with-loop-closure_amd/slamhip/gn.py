@@ -101,6 +101,8 @@ class GaussNewton:
         self.work = dv.empty((n,), np.float64, dev)
         self.status = dv.to_dev(np.zeros(1, np.int32), np.int32, dev)
         self.chi2 = None
+        self._eager_done = False
+        self._graphs = {}
 
     def iterate(self, chi2_out, stream=None):
         """One asynchronous GN iteration; chi2 (before the step) -> chi2_out (device)."""
@@ -111,13 +113,33 @@ class GaussNewton:
             p.n_slots, p.nv, p.W, dv.ptr(self.work), dv.ptr(chi2_out), dv.ptr(self.status),
             dv.stream_handle(stream)), "slam_gn_iteration_f64")
 
-    def run(self, iterations=10, tol=None, stream=None):
-        """Run `iterations` steps; returns the chi2 before every step (host)."""
+    def run(self, iterations=10, tol=None, stream=None, graph=None):
+        """Run `iterations` steps; returns the chi2 before every step (host).
+
+        After one eager run (which also sets the kernels' one-time attributes),
+        the launch sequence of `iterations` steps (~30 kernels per step) is
+        captured once into a HIP graph and replayed (``graph=False`` forces
+        eager launches)."""
         t = dv.torch()
-        chis = t.zeros(max(iterations, 1), dtype=t.float64, device=self.poses.device)
-        for k in range(iterations):
-            self.iterate(chis[k:k + 1], stream)
-        out = chis[:iterations].cpu().numpy()
+        if graph is None:
+            graph = self._eager_done and stream is None and iterations > 0
+        if graph:
+            ent = self._graphs.get(iterations)
+            if ent is None:
+                chis = t.zeros(iterations, dtype=t.float64, device=self.poses.device)
+                g = t.cuda.CUDAGraph()
+                with t.cuda.graph(g):
+                    for k in range(iterations):
+                        self.iterate(chis[k:k + 1])
+                ent = self._graphs[iterations] = (g, chis)
+            g, chis = ent
+            g.replay()
+        else:
+            chis = t.zeros(max(iterations, 1), dtype=t.float64, device=self.poses.device)
+            for k in range(iterations):
+                self.iterate(chis[k:k + 1], stream)
+            self._eager_done = True
+        out = chis[:iterations].cpu().numpy().copy()
         if int(self.status.cpu().numpy()[0]) != 0:
             raise _abi.SlamHipError("Gauss-Newton: H is not positive definite (disconnected graph?)")
         self.chi2 = out

@@ -188,3 +188,16 @@ def test_gn_bcr_block_sizes(shape):
     got, chi = gn.optimize(guess, ea, eb, tf, iterations=3)
     assert np.allclose(chi, ref_chi, rtol=1e-8)
     assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
+
+
+@pytest.mark.gpu
+def test_gn_graph_replay_matches_eager():
+    """The captured HIP graph of k GN steps gives the eager launches' bits."""
+    from slamhip import gn, synthetic
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=25, num_loops=4, n_loops=300)
+    a = gn.GaussNewton(guess, ea, eb, tf)
+    chi_e = np.concatenate([a.run(1, graph=False), a.run(3, graph=False)])
+    b = gn.GaussNewton(guess, ea, eb, tf)
+    chi_g = np.concatenate([b.run(1, graph=False), b.run(3, graph=True)])
+    assert np.array_equal(chi_e, chi_g)
+    assert np.array_equal(a.host_poses(), b.host_poses())

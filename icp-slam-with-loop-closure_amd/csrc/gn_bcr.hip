@@ -31,6 +31,13 @@ constexpr int kBcrMaxWb = 96;
 
 __host__ __device__ inline int64_t bcr_blk(int Wb) { return static_cast<int64_t>(Wb) * Wb; }
 
+// e -> (e / Wb, e % Wb) for e < Wb^2 <= 96^2 without an integer division: the
+// float quotient's fraction stays below 1 - 1/Wb + 1e-3.
+__device__ inline void bcr_rc(int e, int Wb, float inv, int& r, int& c) {
+    r = static_cast<int>(static_cast<float>(e) * inv);
+    c = e - r * Wb;
+}
+
 // Band (row r holds (r, r-d), d = 0..W) -> D_i (full symmetric), E_i, b_i;
 // rows past nv are padded with the identity.
 __global__ void bcr_load_kernel(const double* __restrict__ Hb, const double* __restrict__ rhs, int32_t nv,
@@ -63,39 +70,46 @@ __global__ void bcr_load_kernel(const double* __restrict__ Hb, const double* __r
 
 // Wave 0, lanes 0..15: factor the 16 x 16 diagonal block at k0 in registers
 // (lane i holds row i; pivots and L[c][j] broadcast with v_readlane).
-__device__ inline bool bcr_diag16(double* Cm, int ldc, int k0) {
+__device__ inline bool bcr_diag16(double* Cm, int ldc, int k0, double* rdg) {
     const int lane = threadIdx.x & 63;
     double row[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) row[c] = (lane < 16 && c <= lane) ? Cm[(k0 + lane) * ldc + k0 + c] : 0.0;
     bool bad = false;
+    double rdl = 0.0;   // lane j: 1 / L[j][j]
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const double piv = readlane_d(row[j], j);
         bad |= !(piv > 0.0);
-        const double d = sqrt(piv);
-        if (lane == j) row[j] = d;
-        if (lane > j) row[j] = row[j] / d;
+        const double rd = rsqrt(piv);   // reciprocal pivots: no fp64 division on the chain
+        const double d = piv * rd;
+        if (lane == j) {
+            row[j] = d;
+            rdl = rd;
+        }
+        if (lane > j) row[j] = row[j] * rd;
 #pragma unroll
         for (int c = j + 1; c < 16; ++c) {
             const double lcj = readlane_d(row[j], c);
             if (lane >= c) row[c] = fma(-row[j], lcj, row[c]);
         }
     }
-    if (lane < 16)
+    if (lane < 16) {
 #pragma unroll
         for (int c = 0; c < 16; ++c)
             if (c <= lane) Cm[(k0 + lane) * ldc + k0 + c] = row[c];
+        rdg[k0 + lane] = rdl;
+    }
     return bad;
 }
 
 // Blocked right-looking Cholesky of the LDS tile (lower triangle), all
 // threads; returns through *status on a non-positive pivot.
-__device__ inline void bcr_chol(double* Cm, int ldc, int Wb, int32_t* status) {
+__device__ inline void bcr_chol(double* Cm, int ldc, double* rdg, int Wb, int32_t* status) {
     const int tid = threadIdx.x;
     for (int k0 = 0; k0 < Wb; k0 += 16) {
         if (tid < 64) {
-            const bool bad = bcr_diag16(Cm, ldc, k0);
+            const bool bad = bcr_diag16(Cm, ldc, k0, rdg);
             if (bad && tid == 0 && status) *status = 1;
         }
         __syncthreads();
@@ -111,7 +125,7 @@ __device__ inline void bcr_chol(double* Cm, int ldc, int Wb, int32_t* status) {
                 double v = Cm[r * ldc + k0 + t];
 #pragma unroll
                 for (int q = 0; q < t; ++q) v = fma(-l[q], Cm[(k0 + t) * ldc + k0 + q], v);
-                l[t] = v / Cm[(k0 + t) * ldc + k0 + t];
+                l[t] = v * rdg[k0 + t];
             }
 #pragma unroll
             for (int t = 0; t < 16; ++t) Cm[r * ldc + k0 + t] = l[t];
@@ -157,7 +171,7 @@ __device__ inline void bcr_chol(double* Cm, int ldc, int Wb, int32_t* status) {
 
 // Blocked forward substitution C X = R in place for nc columns of R (LDS,
 // row stride ldr), all threads.
-__device__ inline void bcr_trsm(const double* Cm, int ldc, double* Rm, int ldr, int Wb, int nc) {
+__device__ inline void bcr_trsm(const double* Cm, int ldc, const double* rdg, double* Rm, int ldr, int Wb, int nc) {
     const int tid = threadIdx.x;
     for (int k0 = 0; k0 < Wb; k0 += 16) {
         // diagonal block: one thread per column
@@ -170,7 +184,7 @@ __device__ inline void bcr_trsm(const double* Cm, int ldc, double* Rm, int ldr, 
                 double v = Rm[(k0 + t) * ldr + c];
 #pragma unroll
                 for (int q = 0; q < t; ++q) v = fma(-Cm[(k0 + t) * ldc + k0 + q], x[q], v);
-                x[t] = v / Cm[(k0 + t) * ldc + k0 + t];
+                x[t] = v * rdg[k0 + t];
             }
 #pragma unroll
             for (int t = 0; t < 16; ++t) Rm[(k0 + t) * ldr + c] = x[t];
@@ -220,11 +234,23 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __re
                                                               const double* __restrict__ E, double* __restrict__ Cs,
                                                               double* __restrict__ Xs, double* __restrict__ Ys,
                                                               double* __restrict__ bz, int32_t Wb, int32_t nb,
-                                                              int32_t s, int32_t* __restrict__ status) {
+                                                              int32_t s, int32_t* __restrict__ status,
+                                                              unsigned long long* __restrict__ stamps) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int ldc = Wb + 1, ldr = Wb + 2;
+    // diagnostics: phase s_memtime of workgroup (0, 1), accumulated over levels
+    const bool stamping = stamps && blockIdx.x == 0 && blockIdx.y == 1 && threadIdx.x == 0;
+    unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
+    auto lap = [&](int q) {
+        if (stamping) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            stamps[q] += t1 - t0;
+            t0 = t1;
+        }
+    };
     double* Cm = lds;                                   // [Wb][Wb + 1]
     double* Rm = lds + static_cast<int64_t>(Wb) * ldc;  // [Wb][Wb + 2]
+    double* rdg = Rm + static_cast<int64_t>(Wb) * ldr;  // [Wb] reciprocal diagonal of C
     const int tid = threadIdx.x;
     const int part = blockIdx.y;
     const int i = s + 2 * s * blockIdx.x;
@@ -233,8 +259,10 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __re
     const double* Di = D + i * B2;
     const double* Ep = E + p * B2;                      // A[i, p]: rows of i, columns of p
     const double* Ei = E + i * B2;                      // A[n, i]; A[i, n] = its transpose
+    const float inv = 1.0f / static_cast<float>(Wb);
     for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-        const int r = e / Wb, c = e % Wb;
+        int r, c;
+        bcr_rc(e, Wb, inv, r, c);
         Cm[r * ldc + c] = Di[e];
         if (part == 0) Rm[r * ldr + c] = Ep[e];
         else Rm[r * ldr + c] = n < nb ? Ei[c * Wb + r] : 0.0;
@@ -242,21 +270,30 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __re
     if (part == 1)
         for (int r = tid; r < Wb; r += kBcrThreads) Rm[r * ldr + Wb] = bz[static_cast<int64_t>(i) * Wb + r];
     __syncthreads();
-    bcr_chol(Cm, ldc, Wb, part == 1 ? status : nullptr);
-    bcr_trsm(Cm, ldc, Rm, ldr, Wb, part == 0 ? Wb : Wb + 1);
+    lap(0);
+    bcr_chol(Cm, ldc, rdg, Wb, part == 1 ? status : nullptr);
+    lap(1);
+    bcr_trsm(Cm, ldc, rdg, Rm, ldr, Wb, part == 0 ? Wb : Wb + 1);
+    lap(2);
     if (part == 0) {
         double* Xi = Xs + i * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) Xi[e] = Rm[(e / Wb) * ldr + e % Wb];
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+            int r, c;
+            bcr_rc(e, Wb, inv, r, c);
+            Xi[e] = Rm[r * ldr + c];
+        }
     } else {
         double* Yi = Ys + i * B2;
         double* Ci = Cs + i * B2;
         for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            const int r = e / Wb, c = e % Wb;
+            int r, c;
+            bcr_rc(e, Wb, inv, r, c);
             Yi[e] = Rm[r * ldr + c];
             Ci[e] = c <= r ? Cm[r * ldc + c] : 0.0;
         }
         for (int r = tid; r < Wb; r += kBcrThreads) bz[static_cast<int64_t>(i) * Wb + r] = Rm[r * ldr + Wb];
     }
+    lap(3);
 }
 
 // Even blocks of level s: Schur updates from the odd neighbours i1 = j - s
@@ -283,6 +320,7 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     const bool hE = part == 1 && i2 < nb && j + 2 * s < nb;
     const bool h1 = part == 0 && i1 >= 0, h2 = (part == 0 && i2 < nb) || hE;
     if (!h1 && !h2) return;
+    const float inv = 1.0f / static_cast<float>(Wb);
     const int64_t B2 = bcr_blk(Wb);
     double acc[T][T], accE[T][T];
 #pragma unroll
@@ -295,7 +333,11 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     double bacc = 0.0;   // thread tid < Wb: row tid of the rhs update
     if (h1) {   // D_j -= Y1^T Y1, b_j -= Y1^T z1
         const double* Y1 = Ys + i1 * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) L1[(e / Wb) * ld + e % Wb] = Y1[e];
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+            int r, c;
+            bcr_rc(e, Wb, inv, r, c);
+            L1[r * ld + c] = Y1[e];
+        }
         for (int r = tid; r < Wb; r += kBcrThreads) zv[r] = bz[static_cast<int64_t>(i1) * Wb + r];
         __syncthreads();
         for (int k = 0; k < Wb; ++k) {
@@ -318,8 +360,10 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
         const double* X2 = Xs + i2 * B2;
         const double* Y2 = Ys + i2 * B2;
         for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            L1[(e / Wb) * ld + e % Wb] = X2[e];
-            if (hE) L2[(e / Wb) * ld + e % Wb] = Y2[e];
+            int r, c;
+            bcr_rc(e, Wb, inv, r, c);
+            L1[r * ld + c] = X2[e];
+            if (hE) L2[r * ld + c] = Y2[e];
         }
         // part 1 only needs Y2^T X2; part 0 only X2^T X2
         for (int r = tid; r < Wb; r += kBcrThreads) zv[Wb + r] = bz[static_cast<int64_t>(i2) * Wb + r];
@@ -364,11 +408,11 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
 
 // Backward substitution C^T x = v by one wave, C lower in LDS (stride ldc);
 // v in lanes (rows lane, lane + 64); returns x in the same layout.
-__device__ inline void bcr_backsub_wave(const double* Cm, int ldc, int Wb, double& v0, double& v1) {
+__device__ inline void bcr_backsub_wave(const double* Cm, int ldc, const double* rdg, int Wb, double& v0, double& v1) {
     const int lane = threadIdx.x & 63;
     for (int k = Wb - 1; k >= 0; --k) {
         const double vk = k < 64 ? readlane_d(v0, k) : readlane_d(v1, k - 64);
-        const double xk = vk / Cm[k * ldc + k];
+        const double xk = vk * rdg[k];
         if (lane == k) v0 = xk;
         if (lane + 64 == k) v1 = xk;
         if (lane < k) v0 = fma(-Cm[k * ldc + lane], xk, v0);
@@ -384,15 +428,21 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_top_kernel(double* __restrict
     const int ldc = Wb + 1;
     double* Cm = lds;
     double* y = lds + static_cast<int64_t>(Wb) * ldc;
+    double* rdg = y + Wb;
     const int tid = threadIdx.x;
-    for (int e = tid; e < Wb * Wb; e += kBcrThreads) Cm[(e / Wb) * ldc + e % Wb] = D[e];
+    const float inv = 1.0f / static_cast<float>(Wb);
+    for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+        int r, c;
+        bcr_rc(e, Wb, inv, r, c);
+        Cm[r * ldc + c] = D[e];
+    }
     for (int r = tid; r < Wb; r += kBcrThreads) y[r] = bz[r];
     __syncthreads();
-    bcr_chol(Cm, ldc, Wb, status);
-    bcr_trsm(Cm, ldc, y, 1, Wb, 1);
+    bcr_chol(Cm, ldc, rdg, Wb, status);
+    bcr_trsm(Cm, ldc, rdg, y, 1, Wb, 1);
     if (tid < 64) {
         double v0 = tid < Wb ? y[tid] : 0.0, v1 = tid + 64 < Wb ? y[tid + 64] : 0.0;
-        bcr_backsub_wave(Cm, ldc, Wb, v0, v1);
+        bcr_backsub_wave(Cm, ldc, rdg, Wb, v0, v1);
         if (tid < Wb) x[tid] = v0;
         if (tid + 64 < Wb) x[tid + 64] = v1;
     }
@@ -411,13 +461,20 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
     double* Cm = lds;
     double* vv = lds + static_cast<int64_t>(Wb) * ldc;     // [Wb]
     double* xpn = vv + Wb;                                  // [2][Wb]
+    double* rdg = xpn + 2 * Wb;                             // [Wb]
     const int tid = threadIdx.x;
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
     const int64_t B2 = bcr_blk(Wb);
     const double* Ci = Cs + i * B2;
-    for (int e = tid; e < Wb * Wb; e += kBcrThreads) Cm[(e / Wb) * ldc + e % Wb] = Ci[e];
+    const float inv = 1.0f / static_cast<float>(Wb);
+    for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+        int r, c;
+        bcr_rc(e, Wb, inv, r, c);
+        Cm[r * ldc + c] = Ci[e];
+    }
     for (int k = tid; k < Wb; k += kBcrThreads) {
+        rdg[k] = 1.0 / Ci[static_cast<int64_t>(k) * Wb + k];
         xpn[k] = x[static_cast<int64_t>(p) * Wb + k];
         xpn[Wb + k] = n < nb ? x[static_cast<int64_t>(n) * Wb + k] : 0.0;
     }
@@ -443,7 +500,7 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
     __syncthreads();
     if (tid < 64) {
         double v0 = tid < Wb ? vv[tid] : 0.0, v1 = tid + 64 < Wb ? vv[tid + 64] : 0.0;
-        bcr_backsub_wave(Cm, ldc, Wb, v0, v1);
+        bcr_backsub_wave(Cm, ldc, rdg, Wb, v0, v1);
         double* xi = x + static_cast<int64_t>(i) * Wb;
         if (tid < Wb) xi[tid] = v0;
         if (tid + 64 < Wb) xi[tid + 64] = v1;
@@ -468,7 +525,7 @@ int64_t bcr_work_size(int32_t nv, int32_t W) {
 // Solve H dx = rhs (H in band storage, work of bcr_work_size doubles); *dx_out
 // points at the solution inside `work` (first nv entries).
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
-              double** dx_out, int32_t* status, hipStream_t st) {
+              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps) {
     const int nb = (nv + Wb - 1) / Wb;
     const int64_t B2 = bcr_blk(Wb);
     double* D = work;
@@ -482,9 +539,9 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     const int64_t tot = nb * B2;
     hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs, nv,
                        W, Wb, nb, D, E, bz);
-    const size_t lds_odd = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + static_cast<size_t>(Wb) * (Wb + 2));
+    const size_t lds_odd = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + static_cast<size_t>(Wb) * (Wb + 2) + Wb);
     const size_t lds_even = sizeof(double) * (2 * static_cast<size_t>(Wb) * (Wb + 1) + 2 * static_cast<size_t>(Wb));
-    const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 3 * static_cast<size_t>(Wb));
+    const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 4 * static_cast<size_t>(Wb));
     using EvenFn = void (*)(double*, double*, const double*, const double*, double*, int32_t, int32_t, int32_t);
     static const EvenFn evens[6] = {bcr_even_kernel<1>, bcr_even_kernel<2>, bcr_even_kernel<3>,
                                     bcr_even_kernel<4>, bcr_even_kernel<5>, bcr_even_kernel<6>};
@@ -506,7 +563,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
         hipLaunchKernelGGL(bcr_odd_kernel, dim3(n_odd, 2), dim3(kBcrThreads), lds_odd, st, D, E, Cs, Xs, Ys, bz, Wb,
-                           nb, s, status);
+                           nb, s, status, stamps);
         hipLaunchKernelGGL(even, dim3(n_even, 2), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);

@@ -498,7 +498,7 @@ namespace slamhip {
 int bcr_block_rows(int32_t nv, int32_t W);
 int64_t bcr_work_size(int32_t nv, int32_t W);
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
-              double** dx_out, int32_t* status, hipStream_t st);
+              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps);
 }  // namespace slamhip
 
 using namespace slamhip;
@@ -579,7 +579,7 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
         const int64_t steps = (static_cast<int64_t>(nv) + kGnS - 1) / kGnS;
         double* bwork = gwin + MPw * (MPw + 1) + static_cast<int64_t>(kGnS) * lpw(W) + MPw + steps * (kGnS + W) * kGnS + 8;
         double* dx = nullptr;
-        const int rc = bcr_solve(Hb, rhs, nv, W, Wb, bwork, &dx, status, s);
+        const int rc = bcr_solve(Hb, rhs, nv, W, Wb, bwork, &dx, status, s, g_gn_stamps);
         if (rc != 0) return rc;
         hipLaunchKernelGGL(gn_update_kernel, dim3((N + 255) / 256), dim3(256), 0, s, poses, N, node_col, dx);
         return check_launch("gn kernels");

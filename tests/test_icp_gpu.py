@@ -200,3 +200,55 @@ def test_nn_modes_identical(k):
         assert np.array_equal(o.tf, outs[0].tf) and np.array_equal(o.err, outs[0].err)
         for h0, h1 in zip(outs[0].hist, o.hist):
             assert np.array_equal(h0, h1)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_small_and_degenerate_scans(k, oracle, mode):
+    """Scan sizes around the pruned search's edges (fewer candidates than one
+    window / one 32-chunk, n1 != n2), duplicate points (first-index ties),
+    collinear clouds and a single-point target: iteration counts, transforms
+    and first-iteration correspondences vs the oracle, in every NN mode."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    rng = np.random.default_rng(17)
+    cases = []
+    # (n1 > 1, n2 = 1) is left out of the transform check: every match is the
+    # same point, the centred cross-covariance is rounding noise and the
+    # rotation is undefined (its correspondences are checked below)
+    for n1, n2 in [(1, 1), (1, 7), (5, 9), (17, 23), (24, 25), (33, 31), (40, 64), (65, 97), (130, 129)]:
+        pc2 = rng.uniform(-3, 3, size=(n2, 2))
+        pc1 = pc2[rng.integers(0, n2, n1)] + rng.normal(0, 0.05, size=(n1, 2))
+        cases.append((pc1, pc2))
+    dup = rng.uniform(-2, 2, size=(40, 2))
+    dup = np.concatenate([dup, dup[::3], dup[5:9]])              # exact duplicates in pc2
+    cases.append((dup[:30] + 0.01, dup))
+    line = np.c_[np.linspace(-4, 4, 90), 0.5 * np.linspace(-4, 4, 90)]   # collinear
+    cases.append((line[::2] + [0.02, -0.01], line))
+    scans = [c for pair in cases for c in pair]
+    B = len(cases)
+    src, dst = np.arange(0, 2 * B, 2), np.arange(1, 2 * B, 2)
+    inits = np.stack([np.eye(3)] * B)
+    try:
+        assert lib.slam_icp_set_screen(mode) == 0
+        res = k.icp_batch(scans, src, dst, inits, epsilon=1e-12, max_iters=20, stopping_thresh=1e-14)
+        _, corr, _ = k.icp_step(scans, src, dst, inits)
+    finally:
+        lib.slam_icp_set_screen(2)
+    for b, (pc1, pc2) in enumerate(cases):
+        h, e = oracle.icp(homog(pc1), homog(pc2), np.eye(3), 1e-12, 20, 1e-14)
+        assert res.iters[b] == len(h) - 1, (b, mode)
+        assert np.allclose(res.tf[b], h[-1], rtol=0, atol=1e-9), (b, mode)
+        assert np.array_equal(corr[b], oracle.correspondences(homog(pc1), homog(pc2))), (b, mode)
+    one = rng.uniform(-1, 1, size=(1, 2))
+    _, c1, _ = k.icp_step([rng.uniform(-1, 1, size=(3, 2)), one], [0], [1], np.eye(3)[None])
+    assert c1[0].tolist() == [0, 0, 0]
+
+
+def test_far_coordinates_use_exact_path(k, oracle):
+    """|coordinates| >= 1e18 disable the fp32 screen (finite squares not
+    guaranteed): the kernel falls back to the exact scan for every query."""
+    rng = np.random.default_rng(4)
+    pc2 = rng.uniform(-3, 3, size=(200, 2)) * 1e18
+    pc1 = pc2[:150] * (1 + 1e-9)
+    _, corr, _ = k.icp_step([pc1, pc2], [0], [1], np.eye(3)[None])
+    assert np.array_equal(corr[0], oracle.correspondences(homog(pc1), homog(pc2)))

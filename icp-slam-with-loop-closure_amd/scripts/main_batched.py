@@ -8,13 +8,15 @@ Runs the reference's program flow (``scripts/main.py:66-181`` flags,
 
 and writes the same artefacts under ``--results-dir``:
 ``icp_pose_graph.{pickle,g2o}`` (or ``odometry_pose_graph.*`` with
-``--skip-icp``), ``loop_closure_pose_graph.*``, ``optim.*``.
+``--skip-icp``), ``loop_closure_pose_graph.*``, ``optim.*``, and the occupancy
+grids of src/visualization.py:74-98 (``<name>_og.png``, ``<name>.map`` with
+``--save-map-files``; names odometry / icp / final) built on the GPU.
 
 Inputs: ``dataset`` is an ``.npz`` scan stream (slamhip.dataset.save) or a
 generator spec ``synthetic:<walk|loop>:<n_scans>[:<seed>]``; for ``loop``
 datasets ``--manual-loop-closures auto`` uses the generator's ground-truth
 loop pairs.  Out of scope here (flags accepted, ignored): image-based loop
-closure detection (OpenCV), occupancy-grid maps, figures.
+closure detection (OpenCV) and the matplotlib figures.
 
     python icp-slam-with-loop-closure_amd/scripts/main_batched.py synthetic:loop:2000:3 \\
         --manual-loop-closures auto --results-dir /tmp/results
@@ -55,16 +57,18 @@ def parse(argv=None):
                    help="sgd = the reference's relaxation (default); gn = Gauss-Newton")
     p.add_argument("--gn-iterations", default=10, type=int)
     p.add_argument("--results-dir", default="results")
-    # reference flags for figures / maps / image matching: accepted, not used here
+    p.add_argument("--cell-width", default=0.1, type=float)
+    p.add_argument("--hit-odds", default=5, type=int)
+    p.add_argument("--miss-odds", default=2, type=int)
+    for f in ("--produce-odometry-map", "--skip-occupancy-grid", "--save-map-files", "--occupancy-grid-mle"):
+        p.add_argument(f, action="store_true")
+    # reference flags for figures / image matching: accepted, not used here
     for f, kw in (("--figure-dpi", dict(type=int)), ("--figure-width", dict(type=float)),
                   ("--figure-height", dict(type=float)), ("--image-downsample", dict(type=int)),
                   ("--image-match-error", dict(type=float)), ("--keypoint-n-matches", dict(type=int)),
-                  ("--cell-width", dict(type=float)), ("--hit-odds", dict(type=int)),
-                  ("--miss-odds", dict(type=int)), ("--image-pointcloud-downsample", dict(type=int)),
-                  ("--min-dist-along-path", dict(type=int))):
+                  ("--image-pointcloud-downsample", dict(type=int)), ("--min-dist-along-path", dict(type=int))):
         p.add_argument(f, **kw)
-    for f in ("--produce-odometry-map", "--skip-occupancy-grid", "--save-icp-images", "--no-save-matches",
-              "--no-save-dist-mat", "--save-map-files", "--occupancy-grid-mle"):
+    for f in ("--save-icp-images", "--no-save-matches", "--no-save-dist-mat"):
         p.add_argument(f, action="store_true")
     a = p.parse_args(argv)
     if STAGES.index(a.program_end) < STAGES.index(a.program_start):
@@ -72,6 +76,24 @@ def parse(argv=None):
     if a.program_start != "scan_matching" and not a.pose_graph:
         p.error("starting after scan matching needs --pose-graph")
     return a
+
+
+def save_map(a, poses, scans, name, report):
+    """src/visualization.py:83-98 without the figures: the occupancy grid of
+    `poses` (GPU), optionally its MLE, saved as <name>_og.png (+ <name>.map)."""
+    if a.skip_occupancy_grid:
+        return
+    import src.produce_occupancy_grid as pog
+    t0 = time.perf_counter()
+    og, (min_x, min_y) = pog.produce_occupancy_grid(np.asarray(poses), scans, a.cell_width, kHitOdds=a.hit_odds,
+                                                    kMissOdds=a.miss_odds)
+    if a.occupancy_grid_mle:
+        og = pog.grid_mle(og, unknown_empty=True)
+    pog.save_image(og, os.path.join(a.results_dir, "%s_og.png" % name))
+    if a.save_map_files:
+        pog.save_grid(og, os.path.join(a.results_dir, "%s.map" % name), a.cell_width)
+    report["map_" + name] = {"cells": list(og.shape), "origin": [float(min_x), float(min_y)],
+                             "s": round(time.perf_counter() - t0, 3)}
 
 
 def run(a):
@@ -86,6 +108,8 @@ def run(a):
     odometry = np.asarray(odometry)[a.dataset_start:end]
     scans = list(scans)[a.dataset_start:end]
     report["scans"] = len(scans)
+    if a.produce_odometry_map:
+        save_map(a, odometry, scans, "odometry", report)
 
     pg = None
     if a.program_start == "scan_matching":
@@ -99,6 +123,8 @@ def run(a):
             stem = "icp_pose_graph"
             report["icp_mean_iters"] = float(np.mean(r.iters)) if len(r.iters) else 0.0
         report["scan_matching_s"] = round(time.perf_counter() - t0, 3)
+        if not a.skip_icp:
+            save_map(a, pg.poses, scans, "icp", report)
         pg.save(out(stem + ".pickle"))
         pg.export_g2o(out(stem + ".g2o"))
     if a.program_end == "scan_matching":
@@ -132,6 +158,7 @@ def run(a):
     pipeline.optimize(pg, scans, a.optimization_max_iters, a.icp_max_iters, a.icp_epsilon,
                       icp_recompute=a.icp_recompute, method=a.optimizer, gn_iterations=a.gn_iterations)
     report["optimization_s"] = round(time.perf_counter() - t0, 3)
+    save_map(a, pg.poses, scans, "final", report)
     pg.save(out("optim.pickle"))
     pg.export_g2o(out("optim.g2o"))
     return report

@@ -34,7 +34,7 @@ def to_dev(a, dtype, device=None):
 def empty(shape, dtype, device=None):
     t = require_gpu()
     dev = device if device is not None else default_device()
-    tdt = {np.float64: t.float64, np.int64: t.int64, np.int32: t.int32}[dtype]
+    tdt = {np.float64: t.float64, np.int64: t.int64, np.int32: t.int32, np.int8: t.int8, np.uint8: t.uint8}[dtype]
     return t.empty(shape, dtype=tdt, device=dev)
 
 

@@ -154,6 +154,22 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea,
                           int32_t nv, int32_t W, double* work,
                           double* out_chi2, int32_t* status, void* stream);
 
+/* ---- occupancy grid (src/produce_occupancy_grid.py) ------------------------
+ * pts: packed (x, y) scan points, scan_off (S+1), pose4 (S x 4: cos theta,
+ * sin theta, x, y of each scan's pose; cos/sin as np.cos/np.sin give them).
+ * slam_grid_global_points_f64 replaces construct_global_points (:75-87):
+ * gpts (P x 2) and bounds = (min x, max x, min y, max y) of all of them.
+ * slam_grid_update_i8 replaces update_occupancy_grid / the beam loop of
+ * produce_occupancy_grid (:54-73, bresenham_update :89-121): the int8 grid
+ * (H x W, row = y) is updated in place with the reference's per-beam rule.
+ * work: slam_grid_work_size(S, H, W) BYTES. */
+int64_t slam_grid_work_size(int32_t S, int32_t H, int32_t W);
+int slam_grid_global_points_f64(const double* pts, const int64_t* scan_off, int32_t S, const double* pose4,
+                                double* gpts, double* bounds, void* work, void* stream);
+int slam_grid_update_i8(const double* gpts, const int64_t* scan_off, int32_t S, const double* pose4, int64_t P,
+                        double min_x, double min_y, double cell_width, int32_t H, int32_t W, int32_t k_hit,
+                        int32_t k_miss, int8_t* grid, void* work, void* stream);
+
 /* Diagnostics (kernel-shape sweeps; not needed by callers). */
 int slam_icp_num_instances(void);
 int slam_icp_instance_shape(int i, int* block, int* qpt);

@@ -1,0 +1,106 @@
+"""Occupancy-grid mapper (src/produce_occupancy_grid.py): the order-free
+per-cell rule the kernel relies on (CPU, exhaustive against the sequential
+int8 rule), the oracle on hand-derived rays (CPU), and the HIP path against the
+oracle (GPU).  Parity vs the reference itself is unpinned: the reference module
+imports cv2 (absent), see oracle/occupancy_oracle.py."""
+import numpy as np
+import pytest
+
+import occupancy_oracle as oo
+
+
+def _seq(g0, events, kh, km):
+    g = np.int8(g0)
+    with np.errstate(over="ignore"):
+        for hit in events:
+            if hit:
+                g = np.int8(g + kh if (127 - g) > kh else 127)
+            else:
+                g = np.int8(g - km if (-128 - g) < -km else -128)
+    return int(g)
+
+
+def _closed(g0, m, h, last_hit, kh, km):
+    if m == 0 and h == 0:
+        return g0
+    if h == 0:
+        return -128 if g0 > 0 else max(g0 - m * km, -128)
+    if m == 0:
+        return 127 if g0 < 0 else min(g0 + h * kh, 127)
+    return 127 if last_hit else -128
+
+
+def test_order_free_cell_rule():
+    """The kernel's closed form equals the reference's sequential int8 rule
+    for every start value, odds pair and event sequence up to length 6."""
+    import itertools
+    for kh, km in [(1, 1), (3, 1), (5, 2), (7, 9), (127, 127)]:
+        for g0 in range(-128, 128, 3):
+            for n in range(0, 7):
+                for ev in itertools.product([False, True], repeat=n):
+                    got = _closed(g0, ev.count(False), ev.count(True), ev[-1] if ev else False, kh, km)
+                    assert got == _seq(g0, ev, kh, km), (g0, kh, km, ev)
+
+
+def test_oracle_single_ray():
+    """A horizontal beam of 5 cells: 5 misses (the endpoint's included), then
+    the hit on the endpoint — which is negative by then, so the int8 test
+    wraps and the hit saturates it to 127."""
+    grid = np.zeros((3, 8), dtype=np.int8)
+    oo.ray_update(grid, np.array([0.05, 0.15]), np.array([0.45, 0.15]), 0.0, 0.0, 0.1, 3, 1)
+    assert grid[1].tolist() == [-1, -1, -1, -1, 127, 0, 0, 0]
+    oo.ray_update(grid, np.array([0.05, 0.15]), np.array([0.45, 0.15]), 0.0, 0.0, 0.1, 3, 1)
+    # second beam: the endpoint's miss hits a positive cell (-> -128), its hit a negative one (-> 127)
+    assert grid[1].tolist() == [-2, -2, -2, -2, 127, 0, 0, 0]
+
+
+def _scans(n, beams, seed):
+    from slamhip import synthetic
+    seq = synthetic.make_sequence(n, seed=seed, n_beams=beams)
+    return seq.truth, seq.scans
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cw,kh,km", [(0.1, 3, 1), (0.05, 5, 2)])
+def test_produce_vs_oracle(cw, kh, km):
+    import src.produce_occupancy_grid as pog
+    poses, scans = _scans(6, 181, 3)
+    g, (mx, my) = pog.produce_occupancy_grid(poses, scans, cw, kHitOdds=kh, kMissOdds=km)
+    r, (rx, ry) = oo.produce(poses, scans, cw, k_hit=kh, k_miss=km)
+    assert (mx, my) == (rx, ry) and g.shape == r.shape and g.dtype == np.int8
+    assert np.array_equal(g, r)
+
+
+@pytest.mark.gpu
+def test_update_min_size_and_global_points():
+    import src.produce_occupancy_grid as pog
+    poses, scans = _scans(5, 121, 8)
+    g, (mx, my) = pog.produce_occupancy_grid(poses[:3], scans[:3], 0.1, min_width=30, min_height=25)
+    r, (rx, ry) = oo.produce(poses[:3], scans[:3], 0.1, min_width=30, min_height=25)
+    assert np.array_equal(g, r) and g.shape == (250, 300)
+    pog.update_occupancy_grid(g, poses[3:], scans[3:], 0.1, mx, my)
+    oo.update(r, poses[3:], scans[3:], 0.1, rx, ry)
+    assert np.array_equal(g, r)
+    gp = pog.construct_global_points(poses, scans)
+    rp = oo.global_points(poses, scans)
+    assert max(np.abs(a - b).max() for a, b in zip(gp, rp)) <= 1e-14
+
+
+@pytest.mark.gpu
+def test_bad_odds_raise():
+    import src.produce_occupancy_grid as pog
+    from slamhip._abi import SlamHipError
+    poses, scans = _scans(2, 31, 1)
+    with pytest.raises(SlamHipError):
+        pog.produce_occupancy_grid(poses, scans, 0.1, kHitOdds=0)
+
+
+def test_save_formats(tmp_path):
+    import src.produce_occupancy_grid as pog
+    g = np.array([[-128, 0, 5], [127, -3, 0]], dtype=np.int8)
+    pog.save_grid(g, str(tmp_path / "m.map"), 0.1)
+    lines = (tmp_path / "m.map").read_text().splitlines()
+    assert lines[0] == "0 0 3 2 0.100000" and lines[1].split() == ["127", "-3", "0"]
+    pog.save_image(g, str(tmp_path / "m.png"))
+    assert (tmp_path / "m.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
+    assert pog.grid_mle(g).tolist() == [[-128, 0, 127], [127, -128, 0]]

@@ -90,7 +90,9 @@ def test_cli_end_to_end(tmp_path):
     import main_batched as mb
     import src.pose_graph as pgm
     rep = mb.run(mb.parse(["synthetic:loop:600:4", "--manual-loop-closures", "auto",
-                           "--results-dir", str(tmp_path), "--optimization-max-iters", "5"]))
+                           "--results-dir", str(tmp_path), "--optimization-max-iters", "5", "--save-map-files"]))
+    for f in ("icp_og.png", "final_og.png", "icp.map", "final.map"):
+        assert (tmp_path / f).exists(), f
     assert rep["scans"] == 600 and rep["loop_closures"]["accepted"] >= 1
     for f in ("icp_pose_graph", "loop_closure_pose_graph", "optim"):
         assert (tmp_path / (f + ".pickle")).exists() and (tmp_path / (f + ".g2o")).exists()
@@ -100,5 +102,5 @@ def test_cli_end_to_end(tmp_path):
     # restart from the saved loop-closure graph at the optimisation stage
     rep2 = mb.run(mb.parse(["synthetic:loop:600:4", "--program-start", "optimization", "--pose-graph",
                             str(tmp_path / "loop_closure_pose_graph.pickle"), "--results-dir", str(tmp_path),
-                            "--optimizer", "gn", "--gn-iterations", "3"]))
+                            "--optimizer", "gn", "--gn-iterations", "3", "--skip-occupancy-grid"]))
     assert "optimization_s" in rep2

@@ -1,10 +1,11 @@
 """Config C5 stand-in (BASELINE.json configs[4]): full pipeline on a
 50,000-scan synthetic indoor loop — stage 1 batched ICP odometry, ground-truth
 loop pairs through the manual loop-closure path (scripts/main.py:298-307, one
-batched ICP launch), 50 SGD steps + orientation recompute — timed per stage on
-one MI355X, with bounded CPU-reference checks (the full CPU flow would take
-hours): oracle ICP on a sample of stage-1 and loop pairs, and the first SGD
-steps on the full graph.  GPU only.  Prints one JSON line.
+batched ICP launch), 50 SGD steps + orientation recompute, and the occupancy
+grid of the result — timed per stage on one MI355X, with bounded CPU-reference
+checks (the full CPU flow would take hours): oracle ICP on a sample of stage-1
+and loop pairs, the first SGD steps on the full graph, and the map of the
+first scans.  GPU only.  Prints one JSON line.
 
     python tools/c5_pipeline.py [n_scans] [sgd_check_steps]
 """
@@ -59,6 +60,11 @@ def main():
     solver.orient()
     final = solver.host_poses()
     rep["stage3_sgd50_orient_s"] = round(time.perf_counter() - t0, 3)
+    import src.produce_occupancy_grid as pog
+    t0 = time.perf_counter()
+    og, origin = pog.produce_occupancy_grid(final, seq.scans, 0.1, kHitOdds=5, kMissOdds=2)
+    rep["map_final_s"] = round(time.perf_counter() - t0, 3)
+    rep["map_final_cells"] = list(og.shape)
     rep["drift_vs_truth_before_m"] = float(np.abs(r1.poses[:, :2] - seq.truth[:, :2]).max())
     rep["drift_vs_truth_after_m"] = float(np.abs(final[:, :2] - seq.truth[:, :2]).max())
 
@@ -92,6 +98,12 @@ def main():
     rep["check_sgd"] = {"steps": sgd_check, "max_abs_xy_diff": float(np.abs(got[:, :2] - ref[:, :2]).max()),
                         "cpu_s_per_step": round(t_cpu / max(sgd_check, 1), 2),
                         "cpu_note": "oracle/pgo_oracle.py (vectorised NumPy restatement, bit-exact with the reference)"}
+    import occupancy_oracle as oo
+    sub = slice(0, 6)
+    g_gpu, o_gpu = pog.produce_occupancy_grid(final[sub], seq.scans[sub], 0.1, kHitOdds=5, kMissOdds=2)
+    g_ref, o_ref = oo.produce(final[sub], seq.scans[sub], 0.1, k_hit=5, k_miss=2)
+    rep["check_map"] = {"scans": 6, "identical": bool(np.array_equal(g_gpu, g_ref) and o_gpu == o_ref),
+                        "note": "GPU map vs oracle/occupancy_oracle.py (per-beam restatement) on the first scans"}
     print(json.dumps(rep))
 
 

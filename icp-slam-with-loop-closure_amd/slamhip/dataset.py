@@ -7,8 +7,12 @@ same content — odometry poses (S, 3) and S ragged 2-D scans — from
 * an ``.npz`` written by :func:`save` (``odometry``, ``scan_off``, ``scan_pts``
   and optionally ``loop_pairs``), or
 * a generator spec ``synthetic:<walk|loop>:<n_scans>[:<seed>]`` (SURVEY.md
-  §8(d) generator; ``loop`` also yields ground-truth loop pairs).
+  §8(d) generator; ``loop`` also yields ground-truth loop pairs), or
+* a reference dataset FOLDER holding an LCM ``*.log`` (ODOMETRY / LIDAR
+  channels), read like src/dataloader.py's parse_lcm_log(load_images=False).
 """
+import os
+
 import numpy as np
 
 
@@ -35,6 +39,10 @@ def load(spec):
             seq = synthetic.make_loop_sequence(n, seed=seed)
             return seq.odometry, seq.scans, seq.loop_pairs
         raise ValueError(f"unknown synthetic kind {kind!r} (walk | loop)")
+    if os.path.isdir(spec):
+        import src.dataloader as dl
+        odometry, clouds = dl.parse_lcm_log(spec, load_images=False)
+        return odometry, clouds, None
     with np.load(spec, allow_pickle=False) as z:
         off = z["scan_off"]
         pts = z["scan_pts"]

@@ -71,6 +71,14 @@ __device__ __forceinline__ double uniform_d(double v) {
     return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
+// Lane src's double, in every lane (src wave-uniform).
+__device__ __forceinline__ double bcast_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b & 0xffffffff), src);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), src);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
 __device__ __forceinline__ float uniform_f(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
@@ -218,18 +226,32 @@ __device__ __forceinline__ float box_lb(f32x2 alo, f32x2 ahi, const float4& b) {
 // over all other candidates — exactly what the full screen yields — while
 // skipping candidates that provably cannot change them:
 //   1. window: the kWin sub-chunks (of kSub candidates) around the lane's
-//      predicted match p (last iteration's match) are scanned in full, the QPT
+//      predicted match (last iteration's match) are scanned in full, the QPT
 //      queries interleaved for ILP;
-//   2. group mask: lane l of the wave tests chunks l and l+64 (of kChunk) with
-//      the bounding box of the wave's 64 queries against the wave's largest M2
-//      -> 128-bit mask of chunks that may hold anything below some lane's M2;
-//   3. visits: every sub-chunk of a live chunk that lies outside the lane's
-//      window and whose box is within the lane's current M2 is scanned.
+//   2. clearance: a query whose window is unchanged and whose carried
+//      clearance radius, minus this iteration's motion, still exceeds sqrt(M2)
+//      is done (every non-window candidate is provably farther than M2);
+//   3. group mask: for the remaining ("active") queries of a 64-query group,
+//      lane l tests sub-chunk 64 w + l against the box of the active queries
+//      and their largest M2 -> 64-bit live masks;
+//   4. visits: every live sub-chunk outside the lane's window whose box is
+//      within the lane's current M2 is scanned; the bounds seen on the way
+//      give the next clearance radius.
 // Skipped candidates have d32 >= lower bound > M2 at the time of the test, and
 // M2 only decreases, so (M1, M2, J1) equal the full scan's.
 constexpr int kSub = 8;
 constexpr int kWin = 3;
-constexpr int kBatch = 8;     // live sub-chunks tested per batch
+#ifndef SLAM_BATCH
+#define SLAM_BATCH 4
+#endif
+constexpr int kBatch = SLAM_BATCH;   // live sub-chunks tested per batch
+// waves/SIMD the default 1081-point instances are compiled for (A/B builds override)
+#ifndef SLAM_WPE
+#define SLAM_WPE 4
+#endif
+#ifndef SLAM_WPE320
+#define SLAM_WPE320 1
+#endif
 
 __device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, int& J1) {
     const bool lt = d < M1;
@@ -238,12 +260,25 @@ __device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, 
     M1 = fminf(M1, d);
 }
 
+// Clearance state carried across ICP iterations, one 32-bit word per query:
+// a radius R (fp32, low 9 bits cleared) with the query's window start ws in the
+// low bits.  Invariant after iteration t: every candidate OUTSIDE the window
+// [ws, ws + kWin) lies at Euclidean distance >= R from the query's fp32 point.
+// Packing rounds R down, so the packed radius never exceeds the true bound.
+constexpr uint32_t kWsMask = 511;   // nsub <= kCandCap / kSub = 512
+__device__ __forceinline__ float st_radius(uint32_t s) { return __uint_as_float(s & ~kWsMask); }
+__device__ __forceinline__ int st_ws(uint32_t s) { return static_cast<int>(s & kWsMask); }
+__device__ __forceinline__ uint32_t st_pack(float r, int ws) {
+    r = r >= 0.0f ? fminf(r, 1e30f) * (1.0f - 0x1p-12f) : 0.0f;   // NaN -> 0; 2^11 ulps down > 511
+    return (__float_as_uint(r) & ~kWsMask) | static_cast<uint32_t>(ws);
+}
+
 template <int QPT>
 __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ candf,
                                                  const float4* __restrict__ box8, int nsub,
-                                                 const double4* __restrict__ gbox, const SE2& T,
                                                  const float (&qx)[QPT], const float (&qy)[QPT],
                                                  const bool (&valid)[QPT], const int (&pred)[QPT],
+                                                 uint32_t (&st)[QPT],
                                                  float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
                                                  int& nvisit, bool stamping, unsigned long long (&tsub)[5],
                                                  bool counting, unsigned long long& nev) {
@@ -258,6 +293,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             t0 = t1;
         }
     };
+    // window: kWin sub-chunks centred on the prediction's sub-chunk
     int ws[QPT];
 #pragma unroll
     for (int k = 0; k < QPT; ++k) ws[k] = min(max((pred[k] >> 3) - 1, 0), nsub - kWin);
@@ -278,37 +314,41 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         for (int k = 0; k < QPT; ++k) nev += kWin * kSub * __popcll(__ballot(valid[k]));
     }
     lap(0);
-    // 2. group boxes and largest M2, all groups interleaved
-    // The box of a group's transformed queries is the transformed box of its
-    // original points (gbox, computed once per pair), widened by 1e-6 of the
-    // coordinate magnitude so it also holds their fp32 roundings.
-    float gx0[QPT], gx1[QPT], gy0[QPT], gy1[QPT], gM2[QPT];
+    // 2. clearance test: a query whose window is unchanged and whose carried
+    //    radius R (already reduced by this iteration's motion) satisfies
+    //    R^2 > M2 has every non-window candidate at d32 > M2: its window
+    //    result is the full screen's.  Only the other queries ("active") search
+    //    further; a group without active queries is done.
+    bool act[QPT];
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-        const double4 g = gbox[k];   // (x0, x1, y0, y1) of the group's valid original points
-        const double ax = T.m00 * g.x, bx = T.m00 * g.y, cx = T.m01 * g.z, dx = T.m01 * g.w;
-        const double ay = T.m10 * g.x, by = T.m10 * g.y, cy = T.m11 * g.z, dy = T.m11 * g.w;
-        const double magx = fabs(T.m02) + fmax(fabs(ax), fabs(bx)) + fmax(fabs(cx), fabs(dx));
-        const double magy = fabs(T.m12) + fmax(fabs(ay), fabs(by)) + fmax(fabs(cy), fabs(dy));
-        const double ex = 1e-6 * magx + 1e-30, ey = 1e-6 * magy + 1e-30;
-        gx0[k] = uniform_f(static_cast<float>(T.m02 + fmin(ax, bx) + fmin(cx, dx) - ex));
-        gx1[k] = uniform_f(static_cast<float>(T.m02 + fmax(ax, bx) + fmax(cx, dx) + ex));
-        gy0[k] = uniform_f(static_cast<float>(T.m12 + fmin(ay, by) + fmin(cy, dy) - ey));
-        gy1[k] = uniform_f(static_cast<float>(T.m12 + fmax(ay, by) + fmax(cy, dy) + ey));
-        gM2[k] = wave_max_f(valid[k] ? M2[k] : -INFINITY);
+        const float R = st_radius(st[k]);
+        act[k] = valid[k] && !(ws[k] == st_ws(st[k]) && R * R * (1.0f - 1e-5f) > M2[k]);
     }
     lap(1);
-    // 3. per group, per 64-sub-chunk word: lane l tests sub-chunk 64 w + l
-    //    against the group box -> live mask; each live sub-chunk is tested by
-    //    every lane against its own query (batches of kBatch, independent loads),
-    //    the wave OR of those bits says which sub-chunks to scan.
+    // 3. per group with active queries: the box of the active fp32 queries and
+    //    their largest M2; lane l tests sub-chunk 64 w + l against it -> live
+    //    mask; each live sub-chunk is tested by every active lane against its
+    //    own query (batches of kBatch, independent loads), the wave OR of those
+    //    bits says which sub-chunks to scan.  The smallest bound over the rest
+    //    (non-live sub-chunks: gf; live sub-chunks outside the window: lmin)
+    //    is the new clearance radius.
     const int nw = (nsub + 63) >> 6;
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
+        if (__ballot(act[k]) == 0) continue;   // wave-uniform
+        const float bx0 = wave_min_f(act[k] ? qx[k] : INFINITY);
+        const float bx1 = wave_max_f(act[k] ? qx[k] : -INFINITY);
+        const float by0 = wave_min_f(act[k] ? qy[k] : INFINITY);
+        const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
+        const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
+        float gf = INFINITY, lmin = INFINITY;
         for (int w = 0; w < nw; ++w) {
             const int sl = 64 * w + lane;
             // branch-free (no short-circuit): the LDS reads are not serialised behind exec-mask jumps
-            const bool gl = box_lb(f32x2{gx0[k], gy0[k]}, f32x2{gx1[k], gy1[k]}, box8[min(sl, nsub - 1)]) <= gM2[k];
+            const float glb = box_lb(f32x2{bx0, by0}, f32x2{bx1, by1}, box8[min(sl, nsub - 1)]);
+            const bool gl = glb <= gM2;
+            gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
             uint64_t live = __ballot((sl < nsub) & gl);
             if (stamping) tsub[3] += __popcll(live);
             while (live) {
@@ -330,9 +370,10 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 #pragma unroll
                 for (int u = 0; u < kBatch; ++u) {
                     const int sc = 64 * w + static_cast<int>((scpack >> (6 * u)) & 63);
-                    const bool near = box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, bb[u]) <= M2[k];
-                    const bool nd = valid[k] & ((sc < ws[k]) | (sc >= ws[k] + kWin)) & near;
-                    need |= static_cast<uint32_t>(nd) << u;
+                    const float lb = box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, bb[u]);
+                    const bool out = (sc < ws[k]) | (sc >= ws[k] + kWin);
+                    lmin = out ? fminf(lmin, lb) : lmin;   // a padding slot repeats a real box: harmless
+                    need |= static_cast<uint32_t>(act[k] & out & (lb <= M2[k])) << u;
                 }
                 need &= has;
                 // scan the sub-chunks some lane needs (rolled loop: small code)
@@ -354,6 +395,9 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                 }
             }
         }
+        // lb <= d32 <= (1 + 5u) |q - p|^2, so |q - p| >= sqrt(lb) (1 - 1e-5)
+        const float gfar = wave_min_f(gf);
+        if (act[k]) st[k] = st_pack(sqrtf(fminf(gfar, lmin)) * (1.0f - 1e-5f), ws[k]);
     }
     lap(2);
 }
@@ -382,10 +426,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     const int cap = a.cand_cap;
     // SCREEN only: fp32 copy of the candidates and per-wave fallback queues
     float2* candf = reinterpret_cast<float2*>(cand + cap);
-    int* fq = reinterpret_cast<int*>(candf + cap);          // [WAVES][64*QPT] query ids
-    int* fres = fq + WAVES * 64 * QPT;                       // [WAVES][64*QPT] exact answers
-    float4* box8 = reinterpret_cast<float4*>(fres + WAVES * 64 * QPT);   // PRUNE: [cap/8] sub-chunk boxes
-    double4* gbox = reinterpret_cast<double4*>(box8 + cap / kSub);          // PRUNE: [WAVES][QPT] query boxes
+    float4* box8 = reinterpret_cast<float4*>(candf + cap);   // PRUNE: [cap/8] sub-chunk boxes
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -430,43 +471,49 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
             box8[c] = make_float4(x0, y0, x1, y1);
         }
-#pragma unroll
-        for (int k = 0; k < QPT; ++k) {   // bounding box of each group's valid original points
-            const int i = k * BLOCK + tid;
-            double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
-            if (i < n1) {
-                const double2 p = p1[i];
-                x0 = x1 = p.x;
-                y0 = y1 = p.y;
-            }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                x0 = fmin(x0, __shfl_xor(x0, off, 64));
-                x1 = fmax(x1, __shfl_xor(x1, off, 64));
-                y0 = fmin(y0, __shfl_xor(y0, off, 64));
-                y1 = fmax(y1, __shfl_xor(y1, off, 64));
-            }
-            if (lane == 0) gbox[wave * QPT + k] = make_double4(x0, x1, y0, y1);
-        }
     }
     int bprev[QPT];
+    uint32_t st[QPT];   // PRUNE: clearance state (radius | window start), see st_pack
 #pragma unroll
-    for (int k = 0; k < QPT; ++k) bprev[k] = -1;
+    for (int k = 0; k < QPT; ++k) {
+        bprev[k] = -1;
+        st[k] = 0;
+    }
     int nscan_total = 0;
     bool screen = false;
+    float pmax = 0.0f;   // PRUNE: max |coordinate| of pc1 (motion bound slack)
     if constexpr (SCREEN) {
-        double cm[1] = {cmax};
+        double cm[2] = {cmax, 0.0};
+        if constexpr (PRUNE) {
+            for (int i = tid; i < n1; i += BLOCK) {
+                const double2 p = p1[i];
+                cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));
+            }
+        }
         // block max through the sum slab: max is exact, order-free
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) cm[0] = fmax(cm[0], __shfl_xor(cm[0], off, 64));
-        if (lane == 0) red1[wave] = cm[0];
+        for (int off = 32; off >= 1; off >>= 1) {
+            cm[0] = fmax(cm[0], __shfl_xor(cm[0], off, 64));
+            cm[1] = fmax(cm[1], __shfl_xor(cm[1], off, 64));
+        }
+        if (lane == 0) {
+            red1[wave] = cm[0];
+            red1[WAVES + wave] = cm[1];
+        }
         __syncthreads();
         cmax = red1[0];
+        double pm = red1[WAVES];
 #pragma unroll
-        for (int w = 1; w < WAVES; ++w) cmax = fmax(cmax, red1[w]);
+        for (int w = 1; w < WAVES; ++w) {
+            cmax = fmax(cmax, red1[w]);
+            pm = fmax(pm, red1[WAVES + w]);
+        }
         cmax = uniform_d(cmax);
+        pmax = uniform_f(static_cast<float>(pm) * (1.0f + 1e-6f));
         screen = cmax < 1e18;   // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
     }
+    // PRUNE: this iteration's motion T - T_prev in fp32 and its rounding slack
+    float dT[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dsig = 0.0f;
     const int n2_pad = (n2 + kChunk - 1) / kChunk * kChunk;
 
     SE2 T = load_se2(a.init + 9 * static_cast<int64_t>(b));
@@ -527,6 +574,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     const double ty = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
                     fx[k] = static_cast<float>(tx);
                     fy[k] = static_cast<float>(ty);
+                    if constexpr (PRUNE) {
+                        // carried clearance minus this iteration's motion of the fp32
+                        // query: |q_t - q_{t-1}| <= |dT p| + fp32 rounding of both
+                        // queries and of dT p
+                        const float xf = static_cast<float>(x), yf = static_cast<float>(y);
+                        const float ex = fmaf(dT[1], yf, fmaf(dT[0], xf, dT[2]));
+                        const float ey = fmaf(dT[4], yf, fmaf(dT[3], xf, dT[5]));
+                        const float dl = (sqrtf(fmaf(ey, ey, ex * ex)) +
+                                          1e-6f * (fabsf(fx[k]) + fabsf(fy[k]) + fabsf(ex) + fabsf(ey)) + dsig) *
+                                         (1.0f + 1e-5f);
+                        st[k] = st_pack((st_radius(st[k]) - dl) * (1.0f - 1e-5f), st_ws(st[k]));
+                    }
                     M1[k] = INFINITY;
                     M2[k] = INFINITY;
                     C1[k] = 0;
@@ -542,7 +601,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                                                     : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
                             vq[k] = i < n1;
                         }
-                        nn_window_pruned<QPT>(candf, box8, nsub, gbox + wave * QPT, T, fx, fy, vq, pred, M1, M2, C1,
+                        nn_window_pruned<QPT>(candf, box8, nsub, fx, fy, vq, pred, st, M1, M2, C1,
                                               nscan_total, stamping, tsub, counting, nev);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
@@ -555,7 +614,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 }
                 stamp(0);
                 // ---- certify: the screened winner is the exact fp64 argmin? ---
-                int base = 0;
 #pragma unroll
                 for (int k = 0; k < QPT; ++k) {
                     const int i = k * BLOCK + tid;
@@ -594,53 +652,42 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
                         ok = cq < 1e18 && s2 < 3.0e38 && certify(d1, s2, ab);
                     }
-                    const uint64_t fails = __ballot(!ok);
-                    if (!ok) {
-                        const int pos = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-                                            static_cast<uint32_t>(fails >> 32),
-                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(fails), 0u)));
-                        fq[wave * 64 * QPT + pos] = i;
-                        bi[k] = -1 - pos;   // resolved below
+                    // wave-cooperative exact fp64 scan for each uncertified query of
+                    // this group: the whole wave scans pc2 for it, a (distance, index)
+                    // butterfly leaves the first minimum in every lane, the owner takes it
+                    uint64_t fails = __ballot(!ok);
+                    if (counting) nev += static_cast<unsigned long long>(n2) * __popcll(fails);
+                    while (fails) {
+                        const int src = static_cast<int>(__builtin_ctzll(fails));
+                        fails &= fails - 1;
+                        const double x = bcast_d(qx[k], src), y = bcast_d(qy[k], src);
+                        double bd = INFINITY;
+                        int bj = lane < n2 ? lane : 0x7fffffff;
+                        for (int j = lane; j < n2; j += 64) {
+                            const double2 c = cand[j];
+                            const double d = exact_d2(c.x, c.y, x, y);
+                            if (d < bd) {
+                                bd = d;
+                                bj = j;
+                            }
+                        }
+#pragma unroll
+                        for (int off = 32; off >= 1; off >>= 1) {
+                            const double od = __shfl_xor(bd, off, 64);
+                            const int oj = __shfl_xor(bj, off, 64);
+                            if (od < bd || (od == bd && oj < bj)) {
+                                bd = od;
+                                bj = oj;
+                            }
+                        }
+                        if (lane == src) bi[k] = bj;
                     }
-                    base += __popcll(fails);
-                    if (counting) nev += static_cast<unsigned long long>(n2) * __popcll(fails);   // exact fallback
                 }
                 stamp(1);
-                // ---- wave-cooperative exact fallback for uncertified queries ---
-                for (int t = 0; t < base; ++t) {
-                    const int i = fq[wave * 64 * QPT + t];
-                    const double2 p = p1[i];
-                    const double x = fma(T.m02, 1.0, fma(T.m01, p.y, T.m00 * p.x));
-                    const double y = fma(T.m12, 1.0, fma(T.m11, p.y, T.m10 * p.x));
-                    double bd = INFINITY;
-                    int bj = lane < n2 ? lane : 0x7fffffff;
-                    for (int j = lane; j < n2; j += 64) {
-                        const double2 c = cand[j];
-                        const double d = exact_d2(c.x, c.y, x, y);
-                        if (d < bd) {
-                            bd = d;
-                            bj = j;
-                        }
-                    }
-#pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) {
-                        const double od = __shfl_xor(bd, off, 64);
-                        const int oj = __shfl_xor(bj, off, 64);
-                        if (od < bd || (od == bd && oj < bj)) {
-                            bd = od;
-                            bj = oj;
-                        }
-                    }
-                    if (lane == 0) fres[wave * 64 * QPT + t] = bj;
-                }
             }
-            __syncthreads();   // fres visible to every lane of the wave
             stamp(2);
 #pragma unroll
-            for (int k = 0; k < QPT; ++k) {
-                if (bi[k] < 0) bi[k] = fres[wave * 64 * QPT + (-1 - bi[k])];
-                bprev[k] = k * BLOCK + tid < n1 ? bi[k] : -1;
-            }
+            for (int k = 0; k < QPT; ++k) bprev[k] = k * BLOCK + tid < n1 ? bi[k] : -1;
         } else {
             // ---- exact fp64 scan (src/icp.py:62-63) ---------------------------
             double best[QPT];
@@ -755,6 +802,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             const bool stop = (err < a.epsilon) || (it > a.max_iters) ||
                               (it > 0 && fabs(last_err - err) < a.stopping_thresh);
             last_err = err;
+            if constexpr (PRUNE) {
+                // motion of the next iteration's queries: (Tn - T) p, fp32; dsig bounds
+                // its evaluation error (4u of |dT||p|) and the fp64 rounding of both
+                // transforms (|R| <= 1 + 1e-9, |p| <= pmax)
+                dT[0] = uniform_f(static_cast<float>(Tn.m00 - T.m00));
+                dT[1] = uniform_f(static_cast<float>(Tn.m01 - T.m01));
+                dT[2] = uniform_f(static_cast<float>(Tn.m02 - T.m02));
+                dT[3] = uniform_f(static_cast<float>(Tn.m10 - T.m10));
+                dT[4] = uniform_f(static_cast<float>(Tn.m11 - T.m11));
+                dT[5] = uniform_f(static_cast<float>(Tn.m12 - T.m12));
+                const float rr = fmaxf(fabsf(dT[0]) + fabsf(dT[1]), fabsf(dT[3]) + fabsf(dT[4]));
+                const float tt = fmaxf(fabsf(dT[2]), fabsf(dT[5]));
+                const float big = static_cast<float>(fabs(T.m02) + fabs(T.m12) + fabs(Tn.m02) + fabs(Tn.m12));
+                dsig = uniform_f(1e-6f * (rr * pmax + tt) + 1e-9f * (pmax + big) + 1e-30f);
+            }
             // Tn is identical in every lane: keep it in SGPRs
             T.m00 = uniform_d(Tn.m00); T.m01 = uniform_d(Tn.m01); T.m02 = uniform_d(Tn.m02);
             T.m10 = uniform_d(Tn.m10); T.m11 = uniform_d(Tn.m11); T.m12 = uniform_d(Tn.m12);
@@ -799,7 +861,7 @@ struct Instance {
 static const Instance kInstances[] = {
     SLAM_INST(64, 1, 1),   SLAM_INST(64, 2, 1),   SLAM_INST(64, 4, 1),   SLAM_INST(128, 3, 1),
     SLAM_INST(128, 4, 1),  SLAM_INST(192, 4, 1),  SLAM_INST(192, 6, 1),  SLAM_INST(256, 4, 1),
-    SLAM_INST(256, 5, 4),  SLAM_INST(320, 4, 1),  SLAM_INST(384, 3, 1),  SLAM_INST(512, 3, 1),
+    SLAM_INST(256, 5, SLAM_WPE), SLAM_INST(320, 4, SLAM_WPE320),  SLAM_INST(384, 3, 1),  SLAM_INST(512, 3, 1),
     SLAM_INST(576, 2, 1),  SLAM_INST(512, 4, 1),  SLAM_INST(512, 6, 1),  SLAM_INST(512, 8, 1),
     SLAM_INST(512, 16, 1),
 };
@@ -900,11 +962,9 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     const int mode = max_n2 <= kCandCap ? g_screen : 0;
     size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
     if (mode >= 1)
-        lds += static_cast<size_t>(a.cand_cap) * sizeof(float2) +
-               2 * sizeof(int) * static_cast<size_t>(inst->block) * inst->qpt;
+        lds += static_cast<size_t>(a.cand_cap) * sizeof(float2);
     if (mode == 2)
-        lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
-               static_cast<size_t>(inst->block / 64) * inst->qpt * sizeof(double4);
+        lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4);
     KernelFn fn = mode == 2 ? (step ? inst->step_prune : inst->batch_prune)
                 : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)
                             : (step ? inst->step : inst->batch);

@@ -252,3 +252,59 @@ def test_far_coordinates_use_exact_path(k, oracle):
     pc1 = pc2[:150] * (1 + 1e-9)
     _, corr, _ = k.icp_step([pc1, pc2], [0], [1], np.eye(3)[None])
     assert np.array_equal(corr[0], oracle.correspondences(homog(pc1), homog(pc2)))
+
+
+def _hard_clouds():
+    """Scans that stress the carried clearance of the pruned screen: large
+    first motions followed by small ones, unstructured clouds, exact ties on
+    a lattice, and clustered duplicates."""
+    rng = np.random.default_rng(31)
+    scans, pairs = [], []
+
+    def add(a, b, init):
+        scans.append(a)
+        scans.append(b)
+        pairs.append((len(scans) - 2, len(scans) - 1, init))
+
+    def rot(th, tx=0.0, ty=0.0):
+        return np.array([[np.cos(th), -np.sin(th), tx], [np.sin(th), np.cos(th), ty], [0, 0, 1.0]])
+
+    for th in (0.05, 0.3, 0.8):
+        p2 = rng.uniform(-5, 5, size=(1081, 2))
+        p1 = (p2 - [0.3, -0.2]) @ rot(th)[:2, :2] + rng.normal(0, 0.01, p2.shape)
+        add(p1, p2, np.eye(3))
+    g = np.stack(np.meshgrid(np.arange(33), np.arange(32)), -1).reshape(-1, 2) * 0.25   # exact ties
+    add(g[:1000] + 0.125, g, rot(0.02, 0.1, -0.05))
+    c = np.repeat(rng.uniform(-3, 3, size=(120, 2)), 9, axis=0) + rng.normal(0, 1e-3, (1080, 2))
+    add(c[::-1] + 0.05, c, rot(-0.1))
+    from slamhip import se2, synthetic
+    seq = synthetic.make_sequence(7, seed=77)
+    for i in range(1, 7):   # lidar pairs with a large heading error in the initial guess
+        add(seq.scans[i], seq.scans[i - 1], se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) @ rot(0.4 * (-1) ** i))
+    return scans, pairs
+
+
+def test_nn_modes_identical_hard(k):
+    """The pruned screen (carried clearance, group masks, visits) and the
+    exhaustive fp64 scan give bit-identical transform histories on clouds
+    built to break the pruning bounds."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    scans, pairs = _hard_clouds()
+    src = np.array([p[0] for p in pairs])
+    dst = np.array([p[1] for p in pairs])
+    inits = np.stack([p[2] for p in pairs])
+    outs = []
+    try:
+        for mode in (0, 2):
+            assert lib.slam_icp_set_screen(mode) == 0
+            outs.append(k.icp_batch(scans, src, dst, inits, epsilon=1e-9, max_iters=60, stopping_thresh=1e-12,
+                                    history=True))
+    finally:
+        lib.slam_icp_set_screen(2)
+    a, b = outs
+    assert a.iters.min() > 3
+    assert np.array_equal(a.iters, b.iters)
+    assert np.array_equal(a.tf, b.tf) and np.array_equal(a.err, b.err)
+    for h0, h1 in zip(a.hist, b.hist):
+        assert np.array_equal(h0, h1)

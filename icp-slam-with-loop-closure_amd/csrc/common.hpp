@@ -73,8 +73,8 @@ __device__ __forceinline__ SE2 se2_mul(const SE2& a, const SE2& b) {
 
 // All-lane sum of a wave64 without LDS: pairs and quads by DPP quad_perm,
 // quads of a 16-lane row by DPP row_ror 12 / 8 (lane 0 of each row then holds
-// the row sum), the four rows through SGPRs as (r0+r1)+(r2+r3).  Every lane
-// returns identical bits.
+// the row sum), the four rows combined as (r0+r1)+(r2+r3) by row swaps.  Lane 0
+// holds the result (other lanes may differ in rounding; callers use lane 0).
 #define SLAM_DPP_D(v, ctrl)                                                                            \
     __longlong_as_double(                                                                              \
         (static_cast<long long>(__builtin_amdgcn_update_dpp(                                           \
@@ -94,7 +94,20 @@ __device__ __forceinline__ double wave_sum(double v) {
     v += SLAM_DPP_D(v, 0x4E);    // xor 2
     v += SLAM_DPP_D(v, 0x12C);   // row_ror 12
     v += SLAM_DPP_D(v, 0x128);   // row_ror 8
-    return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+    // rows: (r0 + r1) in rows 0-1, (r2 + r3) in rows 2-3 (gfx950 v_permlane16_swap),
+    // then the halves (v_permlane32_swap): lane 0 holds (r0 + r1) + (r2 + r3)
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(b), static_cast<unsigned>(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(b >> 32), static_cast<unsigned>(b >> 32),
+                                                     false, false);
+    v = __longlong_as_double((static_cast<long long>(hi[0]) << 32) | lo[0]) +
+        __longlong_as_double((static_cast<long long>(hi[1]) << 32) | lo[1]);
+    const long long c = __double_as_longlong(v);
+    const auto lo2 = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(c), static_cast<unsigned>(c), false, false);
+    const auto hi2 = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(c >> 32), static_cast<unsigned>(c >> 32),
+                                                      false, false);
+    return __longlong_as_double((static_cast<long long>(hi2[0]) << 32) | lo2[0]) +
+           __longlong_as_double((static_cast<long long>(hi2[1]) << 32) | lo2[1]);
 }
 #undef SLAM_DPP_D
 

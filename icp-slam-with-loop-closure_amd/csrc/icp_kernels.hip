@@ -61,6 +61,14 @@ struct IcpArgs {
     unsigned long long* stamps;
     // diagnostics: total candidate evaluations performed, all lanes (NULL = off)
     unsigned long long* evals;
+    // phased scheduling (batch mode): workgroup -> pair map (NULL = identity),
+    // iterations per pair in this launch (0 = to completion), resume from the
+    // state a previous phase saved in out_tf / out_err / out_iters, and the
+    // per-pair sort key written at a pause
+    const int32_t* order;
+    int32_t phase_cap;
+    int32_t resume;
+    float* sched_key;
 };
 
 // A wave-uniform double moved to SGPRs (v_readfirstlane of both halves).
@@ -149,40 +157,67 @@ __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf
     }
 }
 
-// Wave-wide min / max without LDS: DPP butterflies inside each 16-lane row,
-// then the four row results through SGPRs (v_readlane).
+// Wave-wide min / max / or without LDS or SGPR round trips: DPP butterflies
+// inside each 16-lane row, then the gfx950 row swaps (v_permlane16_swap pairs
+// rows 0-1 and 2-3, v_permlane32_swap the two halves).  Every lane returns the
+// result.
 #define SLAM_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
-__device__ __forceinline__ float wave_min_f(float v) {
-    v = fminf(v, SLAM_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
-    v = fminf(v, SLAM_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
-    v = fminf(v, SLAM_DPP(v, 0x124));   // row_ror:4
-    v = fminf(v, SLAM_DPP(v, 0x128));   // row_ror:8
+#ifndef SLAM_PERMLANE
+#define SLAM_PERMLANE 1
+#endif
+#if !SLAM_PERMLANE   // A/B reference: the four row results through SGPRs
+__device__ __forceinline__ float cross_rows_min(float v) {
     const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
     const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
     const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
     return fminf(fminf(r0, r1), fminf(r2, r3));
 }
-__device__ __forceinline__ float wave_max_f(float v) {
-    v = fmaxf(v, SLAM_DPP(v, 0xB1));
-    v = fmaxf(v, SLAM_DPP(v, 0x4E));
-    v = fmaxf(v, SLAM_DPP(v, 0x124));
-    v = fmaxf(v, SLAM_DPP(v, 0x128));
+__device__ __forceinline__ float cross_rows_max(float v) {
     const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
     const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
     const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
     return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
+#else
+__device__ __forceinline__ float cross_rows_min(float v) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fminf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float cross_rows_max(float v) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+#endif
+__device__ __forceinline__ float wave_min_f(float v) {
+    v = fminf(v, SLAM_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
+    v = fminf(v, SLAM_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
+    v = fminf(v, SLAM_DPP(v, 0x124));   // row_ror:4
+    v = fminf(v, SLAM_DPP(v, 0x128));   // row_ror:8
+    return cross_rows_min(v);
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+    v = fmaxf(v, SLAM_DPP(v, 0xB1));
+    v = fmaxf(v, SLAM_DPP(v, 0x4E));
+    v = fmaxf(v, SLAM_DPP(v, 0x124));
+    v = fmaxf(v, SLAM_DPP(v, 0x128));
+    return cross_rows_max(v);
+}
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
     v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
     v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
     v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x124, 0xF, 0xF, false));
     v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x128, 0xF, 0xF, false));
-    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0) |
-                                 __builtin_amdgcn_readlane(static_cast<int>(v), 16) |
-                                 __builtin_amdgcn_readlane(static_cast<int>(v), 32) |
-                                 __builtin_amdgcn_readlane(static_cast<int>(v), 48));
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = p[0] | p[1];
+    const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    // wave-uniform by construction: move to an SGPR for the scalar loop over its bits
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(q[0] | q[1])));
 }
 #undef SLAM_DPP
 
@@ -240,7 +275,16 @@ __device__ __forceinline__ float box_lb(f32x2 alo, f32x2 ahi, const float4& b) {
 // Skipped candidates have d32 >= lower bound > M2 at the time of the test, and
 // M2 only decreases, so (M1, M2, J1) equal the full scan's.
 constexpr int kSub = 8;
-constexpr int kWin = 3;
+#ifndef SLAM_WIN
+#define SLAM_WIN 4
+#endif
+#ifndef SLAM_ABLATE
+#define SLAM_ABLATE 0   // diagnostics only (tools/ab_fixed.py): 1 no visits, 2 no certification, 4 no block sums, 8 no clearance
+#endif
+#ifndef SLAM_KEEPQ
+#define SLAM_KEEPQ 0
+#endif
+constexpr int kWin = SLAM_WIN;
 #ifndef SLAM_BATCH
 #define SLAM_BATCH 4
 #endif
@@ -296,7 +340,11 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     // window: kWin sub-chunks centred on the prediction's sub-chunk
     int ws[QPT];
 #pragma unroll
-    for (int k = 0; k < QPT; ++k) ws[k] = min(max((pred[k] >> 3) - 1, 0), nsub - kWin);
+    for (int k = 0; k < QPT; ++k) {
+        // sub-chunks before the predicted one: even windows lean to the nearer half
+        const int lo = (kWin & 1) ? kWin / 2 : kWin / 2 - ((pred[k] & (kSub - 1)) >= kSub / 2 ? 1 : 0);
+        ws[k] = min(max((pred[k] >> 3) - lo, 0), nsub - kWin);
+    }
     // 1. windows (J1 holds the offset inside the window until the end of the loop)
 #pragma unroll 2
     for (int t = 0; t < kWin * kSub; t += 2) {
@@ -324,6 +372,12 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     for (int k = 0; k < QPT; ++k) {
         const float R = st_radius(st[k]);
         act[k] = valid[k] && !(ws[k] == st_ws(st[k]) && R * R * (1.0f - 1e-5f) > M2[k]);
+#if SLAM_ABLATE & 1
+        act[k] = false;
+#endif
+#if SLAM_ABLATE & 8
+        act[k] = valid[k];
+#endif
     }
     lap(1);
     // 3. per group with active queries: the box of the active fp32 queries and
@@ -428,10 +482,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     float2* candf = reinterpret_cast<float2*>(cand + cap);
     float4* box8 = reinterpret_cast<float4*>(candf + cap);   // PRUNE: [cap/8] sub-chunk boxes
 
-    const int b = blockIdx.x;
+    // pair of this workgroup: launch order or the scheduler's order
+    const int b = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+    // resumed phase: out_iters holds -(iterations done) for a paused pair and
+    // the final count for a finished one (nothing left to do)
+    int it0 = 0;
+    if (a.resume) {
+        const int s = a.out_iters[b];
+        if (s > 0) return;   // uniform: the whole workgroup leaves
+        it0 = -s;
+    }
     const int s1 = a.src_scan[b];
     const int s2 = a.dst_scan[b];
     const int64_t o1 = a.scan_off[s1];
@@ -516,7 +579,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     float dT[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dsig = 0.0f;
     const int n2_pad = (n2 + kChunk - 1) / kChunk * kChunk;
 
-    SE2 T = load_se2(a.init + 9 * static_cast<int64_t>(b));
+    // a resumed pair continues from its saved state: the transform and the
+    // previous error (the ICP loop carries nothing else that affects results)
+    SE2 T = load_se2((it0 > 0 ? a.out_tf : a.init) + 9 * static_cast<int64_t>(b));
     if (a.rotation_only) {   // src/icp.py:60-61 zeroes previous_transform[:2, 2]
         T.m02 = 0.0;
         T.m12 = 0.0;
@@ -524,10 +589,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     double* hist = (!STEP && a.hist_stride > 0)
                        ? a.out_hist + static_cast<int64_t>(b) * a.hist_stride * 9
                        : nullptr;
-    if (hist && tid == 0) store_se2(hist, T);
+    if (hist && tid == 0 && it0 == 0) store_se2(hist, T);
+    double last_err = it0 > 0 ? a.out_err[b] : 0.0;
     __syncthreads();
 
-    double last_err = 0.0;
     unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[5] = {0, 0, 0, 0, 0};
 
     const bool stamping = a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
@@ -548,7 +613,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         }
     };
     stamp(-1);
-    for (int it = 0;; ++it) {
+    for (int it = it0;; ++it) {
         // An opaque copy of the thread index per iteration: query addresses and
         // masks derived from it are recomputed (2 VALU) instead of hoisted out
         // of the loop and spilled to scratch.
@@ -574,6 +639,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     const double ty = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
                     fx[k] = static_cast<float>(tx);
                     fy[k] = static_cast<float>(ty);
+#if SLAM_KEEPQ
+                    qx[k] = tx;
+                    qy[k] = ty;
+#endif
                     if constexpr (PRUNE) {
                         // carried clearance minus this iteration's motion of the fp32
                         // query: |q_t - q_{t-1}| <= |dT p| + fp32 rounding of both
@@ -617,6 +686,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 #pragma unroll
                 for (int k = 0; k < QPT; ++k) {
                     const int i = k * BLOCK + tid;
+#if !SLAM_KEEPQ
                     double x = 0.0, y = 0.0;
                     if (i < n1) {
                         const double2 p = p1[i];
@@ -625,6 +695,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     }
                     qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));   // bit-identical to above
                     qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+#endif
                     // winning chunk: first index reaching the chunk minimum + runner-up
                     float b2 = INFINITY;
                     int j1 = C1[k];
@@ -651,6 +722,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
                         const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
                         ok = cq < 1e18 && s2 < 3.0e38 && certify(d1, s2, ab);
+#if SLAM_ABLATE & 2
+                        ok = true;
+#endif
                     }
                     // wave-cooperative exact fp64 scan for each uncertified query of
                     // this group: the whole wave scans pc2 for it, a (distance, index)
@@ -740,7 +814,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 v[4] += exact_d2(m.x, m.y, qx[k], qy[k]);   // (pc1_t - pc2[corr])**2 of the row
             }
         }
+#if !(SLAM_ABLATE & 4)
         block_sum<5, WAVES>(v, red0);
+#endif
         const double n = static_cast<double>(n1);
         const double mux = v[0] / n, muy = v[1] / n;     // pc1_avg
         const double mvx = v[2] / n, mvy = v[3] / n;     // pc2_avg
@@ -761,7 +837,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 s[3] = fma(ya, yb, s[3]);
             }
         }
+#if !(SLAM_ABLATE & 4)
         block_sum<4, WAVES>(s, red1);
+#else
+        s[0] = uniform_d(s[0]); s[1] = uniform_d(s[1]); s[2] = uniform_d(s[2]); s[3] = uniform_d(s[3]);
+        v[0] = uniform_d(v[0]); v[1] = uniform_d(v[1]); v[2] = uniform_d(v[2]); v[3] = uniform_d(v[3]); v[4] = uniform_d(v[4]);
+#endif
 
         // ---- closed-form 2x2 Kabsch: R maximising tr(R S) ---------------------
         // Equals V diag(1, det(V U^T)) U^T of the reference's SVD route.
@@ -799,8 +880,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         } else {
             if (hist && tid == 0) store_se2(hist + 9 * (it + 1), Tn);
             // src/icp.py:86-95 (identical in every thread -> uniform exit)
+            const double derr = fabs(last_err - err);
             const bool stop = (err < a.epsilon) || (it > a.max_iters) ||
-                              (it > 0 && fabs(last_err - err) < a.stopping_thresh);
+                              (it > 0 && derr < a.stopping_thresh);
             last_err = err;
             if constexpr (PRUNE) {
                 // motion of the next iteration's queries: (Tn - T) p, fp32; dsig bounds
@@ -827,6 +909,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
                     a.out_iters[b] = it + 1;
+                }
+                return;
+            }
+            if (a.phase_cap > 0 && it + 1 - it0 >= a.phase_cap) {
+                // pause (scheduler phase boundary): save the loop state; the
+                // last error change orders the survivors for the next phase
+                flush_stamps();
+                if (counting && lane == 0) atomicAdd(a.evals, nev);
+                if (tid == 0) {
+                    store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                    a.out_err[b] = err;
+                    a.out_iters[b] = -(it + 1);
+                    a.sched_key[b] = static_cast<float>(derr);
                 }
                 return;
             }
@@ -974,6 +1069,90 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     return check_launch(step ? "icp_step kernel" : "icp_batch kernel");
 }
 
+// ---------------------------------------------------------------------------
+// Phased scheduling of a large batch.  ICP iteration counts have a long tail
+// (C3: mean 18, p99 36, max 102), and a slow pair that happens to start late
+// keeps the GPU waiting (natural order 8.5 ms vs 5.0 ms for the same pairs
+// sorted by their iteration counts).  Phase 1 runs every pair for kProbe
+// iterations and pauses the unfinished ones; their last error change |dE|
+// (large = far from the |dE| < stopping_thresh exit) orders phase 2, longest
+// first, by a 256-bucket counting sort on log2 |dE| (order within a bucket is
+// arbitrary and irrelevant: pairs are independent and every result is
+// bit-identical to the single-launch run).
+// ---------------------------------------------------------------------------
+constexpr int kSchedBuckets = 256;
+static int g_sched_probe = 5;          // phase-1 iterations (0: single launch; 4-6 best on C3)
+static int g_sched_min_pairs = 2048;   // batches below this fit the GPU in ~2 waves
+
+__global__ __launch_bounds__(256) void sched_count_kernel(const int32_t* __restrict__ iters,
+                                                          const float* __restrict__ key, int32_t B,
+                                                          float thresh, int32_t* __restrict__ hist,
+                                                          int32_t* __restrict__ bucket) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    int q = kSchedBuckets;   // finished pairs go last (their workgroups exit at once)
+    if (iters[b] <= 0) {
+        const float l = log2f(fmaxf(key[b] / thresh, 1e-30f));   // 8 buckets per octave, 2^12 -> 0
+        q = min(max(static_cast<int>(floorf(96.0f - 8.0f * l)), 0), kSchedBuckets - 1);
+    }
+    bucket[b] = q;
+    atomicAdd(&hist[q], 1);
+}
+
+__global__ __launch_bounds__(64) void sched_scan_kernel(int32_t* __restrict__ hist) {
+    if (threadIdx.x != 0) return;   // 257 counters: one lane is plenty
+    int s = 0;
+    for (int q = 0; q <= kSchedBuckets; ++q) {
+        const int c = hist[q];
+        hist[q] = s;
+        s += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void sched_scatter_kernel(const int32_t* __restrict__ bucket, int32_t B,
+                                                            int32_t* __restrict__ offs,
+                                                            int32_t* __restrict__ order) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    order[atomicAdd(&offs[bucket[b]], 1)] = b;
+}
+
+static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2, void* stream) {
+    const int probe = g_sched_probe;
+    if (probe <= 0 || B < g_sched_min_pairs || args.max_iters + 2 <= probe)
+        return launch(false, args, B, max_n1, max_n2, stream);
+    hipStream_t s = as_stream(stream);
+    const size_t nb = static_cast<size_t>(B);
+    const size_t bytes = (kSchedBuckets + 1) * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float));
+    void* ws = nullptr;
+    if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
+    int32_t* hist = static_cast<int32_t*>(ws);
+    int32_t* bucket = hist + kSchedBuckets + 1;
+    int32_t* order = bucket + nb;
+    float* key = reinterpret_cast<float*>(order + nb);
+    IcpArgs a = args;
+    a.phase_cap = probe;
+    a.sched_key = key;
+    int rc = launch(false, a, B, max_n1, max_n2, stream);
+    if (rc == 0) {
+        const int g = (B + 255) / 256;
+        const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
+        (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
+        hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
+        hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);
+        hipLaunchKernelGGL(sched_scatter_kernel, dim3(g), dim3(256), 0, s, bucket, B, hist, order);
+        rc = check_launch("icp scheduler kernels");
+    }
+    if (rc == 0) {
+        a.phase_cap = 0;
+        a.resume = 1;
+        a.order = order;
+        rc = launch(false, a, B, max_n1, max_n2, stream);
+    }
+    (void)hipFreeAsync(ws, s);
+    return rc;
+}
+
 }  // namespace slamhip
 
 using namespace slamhip;
@@ -1005,6 +1184,15 @@ int slam_icp_set_stamps(void* dev_buf) {
 }
 int slam_icp_set_eval_counter(void* dev_u64) {
     g_icp_evals = reinterpret_cast<unsigned long long*>(dev_u64);
+    return ok();
+}
+// Phased scheduling of large batches (see launch_batch): phase-1 iterations
+// (0 = one launch) and the smallest batch it applies to.  Results do not
+// depend on it (tests/test_icp_gpu.py::test_schedule_is_invisible).
+int slam_icp_set_schedule(int probe_iters, int min_pairs) {
+    if (probe_iters < 0 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: negative argument");
+    g_sched_probe = probe_iters;
+    g_sched_min_pairs = min_pairs;
     return ok();
 }
 int slam_icp_set_screen(int mode) {
@@ -1045,7 +1233,7 @@ int slam_icp_batch_f64(const double* pts, const int64_t* scan_off, const int32_t
     a.out_tf = out_tf;
     a.out_err = out_err;
     a.out_iters = out_iters;
-    return launch(false, a, B, max_n1, max_n2, stream);
+    return launch_batch(a, B, max_n1, max_n2, stream);
 }
 
 int slam_icp_step_f64(const double* pts, const int64_t* scan_off, const int32_t* src_scan,

@@ -66,6 +66,8 @@ int slam_icp_max_query_points(void);
  *   out_iters int32[B]       number of ICP iterations k (len(transforms) - 1)
  * Stopping rules are the reference's: err < epsilon; iteration > max_iters;
  * |last_err - err| < stopping_thresh from the second iteration on.
+ * Batches of >= 2048 pairs run in two phases (slam_icp_set_schedule) with a
+ * transient stream-ordered workspace of 12 B/pair (hipMallocAsync/FreeAsync).
  */
 int slam_icp_batch_f64(const double* pts, const int64_t* scan_off,
                        const int32_t* src_scan, const int32_t* dst_scan,
@@ -179,6 +181,12 @@ int slam_icp_selected_instance(int max_n1);
  * screen with exact pruning (per-lane windows + sub-chunk boxes, default);
  * identical results. */
 int slam_icp_set_screen(int mode);
+/* Phased scheduling of slam_icp_batch_f64 for batches of >= min_pairs pairs:
+ * every pair runs probe_iters iterations, then the unfinished ones resume in
+ * order of their last error change (slowest-converging first), so the long
+ * tail of iteration counts does not start late.  probe_iters = 0: one launch.
+ * Defaults (5, 2048).  Results are identical either way. */
+int slam_icp_set_schedule(int probe_iters, int min_pairs);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver: 0 auto (block cyclic reduction when the band allows it),
  * 1 band Cholesky, 2 block cyclic reduction (falls back to 1 if not allowed). */

@@ -308,3 +308,35 @@ def test_nn_modes_identical_hard(k):
     assert np.array_equal(a.tf, b.tf) and np.array_equal(a.err, b.err)
     for h0, h1 in zip(a.hist, b.hist):
         assert np.array_equal(h0, h1)
+
+
+def test_schedule_is_invisible(k):
+    """The phased scheduler (probe phase, pause, re-ordered resume) returns
+    bit-identical transforms, errors, iteration counts and histories to one
+    launch, for every probe length, including pairs that stop inside the
+    probe phase, exactly at its end, and with history recording."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 300
+    seq, inits = _sequence_pairs(n, seed=12, n_beams=361)
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    outs = []
+    try:
+        for probe in (0, 1, 3, 8, 17):
+            assert lib.slam_icp_set_schedule(probe, 1) == 0
+            outs.append(k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True))
+        assert lib.slam_icp_set_schedule(5, 1) == 0   # rotation-only and a max_iters stop inside phase 2
+        outs.append(k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=6, rotation_only=True))
+        assert lib.slam_icp_set_schedule(0, 1) == 0
+        ref_ro = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=6, rotation_only=True)
+    finally:
+        lib.slam_icp_set_schedule(5, 2048)
+    a = outs[0]
+    assert a.iters.min() < 8 < a.iters.max()
+    for o in outs[1:-1]:
+        assert np.array_equal(o.iters, a.iters)
+        assert np.array_equal(o.tf, a.tf) and np.array_equal(o.err, a.err)
+        for h0, h1 in zip(a.hist, o.hist):
+            assert np.array_equal(h0, h1)
+    assert np.array_equal(outs[-1].tf, ref_ro.tf) and np.array_equal(outs[-1].iters, ref_ro.iters)
+    assert np.array_equal(outs[-1].err, ref_ro.err)

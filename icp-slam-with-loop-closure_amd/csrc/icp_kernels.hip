@@ -278,6 +278,9 @@ constexpr int kSub = 8;
 #ifndef SLAM_WIN
 #define SLAM_WIN 4
 #endif
+#ifndef SLAM_HOIST
+#define SLAM_HOIST 0
+#endif
 #ifndef SLAM_ABLATE
 #define SLAM_ABLATE 0   // diagnostics only (tools/ab_fixed.py): 1 no visits, 2 no certification, 4 no block sums, 8 no clearance
 #endif
@@ -388,14 +391,30 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     //    (non-live sub-chunks: gf; live sub-chunks outside the window: lmin)
     //    is the new clearance radius.
     const int nw = (nsub + 63) >> 6;
+#if SLAM_HOIST
+    // boxes of every group at once: independent reduction chains interleave
+    float hb[QPT][5];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+        hb[k][0] = wave_min_f(act[k] ? qx[k] : INFINITY);
+        hb[k][1] = wave_max_f(act[k] ? qx[k] : -INFINITY);
+        hb[k][2] = wave_min_f(act[k] ? qy[k] : INFINITY);
+        hb[k][3] = wave_max_f(act[k] ? qy[k] : -INFINITY);
+        hb[k][4] = wave_max_f(act[k] ? M2[k] : -INFINITY);
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
         if (__ballot(act[k]) == 0) continue;   // wave-uniform
+#if SLAM_HOIST
+        const float bx0 = hb[k][0], bx1 = hb[k][1], by0 = hb[k][2], by1 = hb[k][3], gM2 = hb[k][4];
+#else
         const float bx0 = wave_min_f(act[k] ? qx[k] : INFINITY);
         const float bx1 = wave_max_f(act[k] ? qx[k] : -INFINITY);
         const float by0 = wave_min_f(act[k] ? qy[k] : INFINITY);
         const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
         const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
+#endif
         float gf = INFINITY, lmin = INFINITY;
         for (int w = 0; w < nw; ++w) {
             const int sl = 64 * w + lane;
@@ -921,7 +940,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
                     a.out_iters[b] = -(it + 1);
+#if SLAM_SCHED_KEY == 1
+                    a.sched_key[b] = static_cast<float>(err);
+#else
                     a.sched_key[b] = static_cast<float>(derr);
+#endif
                 }
                 return;
             }
@@ -1081,6 +1104,9 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
+#ifndef SLAM_SCHED_KEY
+#define SLAM_SCHED_KEY 0   // 0: last error change, 1: error level (A/B)
+#endif
 static int g_sched_probe = 5;          // phase-1 iterations (0: single launch; 4-6 best on C3)
 static int g_sched_min_pairs = 2048;   // batches below this fit the GPU in ~2 waves
 
@@ -1092,8 +1118,8 @@ __global__ __launch_bounds__(256) void sched_count_kernel(const int32_t* __restr
     if (b >= B) return;
     int q = kSchedBuckets;   // finished pairs go last (their workgroups exit at once)
     if (iters[b] <= 0) {
-        const float l = log2f(fmaxf(key[b] / thresh, 1e-30f));   // 8 buckets per octave, 2^12 -> 0
-        q = min(max(static_cast<int>(floorf(96.0f - 8.0f * l)), 0), kSchedBuckets - 1);
+        const float l = log2f(fmaxf(key[b] / thresh, 1e-30f));   // 8 buckets per octave, 2^16 -> 0
+        q = min(max(static_cast<int>(floorf(128.0f - 8.0f * l)), 0), kSchedBuckets - 1);
     }
     bucket[b] = q;
     atomicAdd(&hist[q], 1);
@@ -1136,7 +1162,11 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     int rc = launch(false, a, B, max_n1, max_n2, stream);
     if (rc == 0) {
         const int g = (B + 255) / 256;
+#if SLAM_SCHED_KEY == 1
+        const float thr = 1.0f;
+#else
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
+#endif
         (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
         hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
         hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);

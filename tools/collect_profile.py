@@ -18,6 +18,24 @@ def main(tag):
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "icp_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    # one ICP batch = phase-1 + phase-2 launches of icp_kernel + 3 scheduler
+    # kernels (slam_icp_batch_f64 with >= 2048 pairs): per-batch time from the trace
+    batch = {"icp_kernel_calls": 0, "icp_kernel_total_ns": 0.0, "sched_batches": 0, "sched_total_ns": 0.0}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "icp_kernel_stats.csv"))):
+        if "icp_kernel" in r["Name"]:
+            batch["icp_kernel_calls"] += int(r["Calls"])
+            batch["icp_kernel_total_ns"] += float(r["TotalDurationNs"])
+        elif "sched_" in r["Name"]:
+            batch["sched_total_ns"] += float(r["TotalDurationNs"])
+            if "sched_scan_kernel" in r["Name"]:
+                batch["sched_batches"] += int(r["Calls"])
+    nb = batch["sched_batches"] or batch["icp_kernel_calls"]
+    batch["batches"] = nb
+    batch["per_batch_ms"] = (batch["icp_kernel_total_ns"] + batch["sched_total_ns"]) / max(nb, 1) / 1e6
+    batch["note"] = ("bench.py --steps 3 --warmup 1 under rocprofv3 --kernel-trace --stats: warmup + 3 timed + 1 "
+                     "eval-counting batch; per_batch_ms is the device time of one slam_icp_batch_f64 call")
+    json.dump(batch, open(os.path.join(dst, f"{tag}_icp_batch_rocprof.json"), "w"), indent=1)
+    print(json.dumps(batch, indent=1))
     vals = {}
     rows_out = []
     for names, sub in ((("FETCH_SIZE",), "pmc_fetch"), (("WRITE_SIZE",), "pmc_write"),
@@ -40,7 +58,7 @@ def main(tag):
     write = vals["WRITE_SIZE"] * 1024
     out = {"icp_batch_bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch, "write_bytes": write,
            "raw_FETCH_SIZE_KiB": vals["FETCH_SIZE"], "raw_WRITE_SIZE_KiB": vals["WRITE_SIZE"],
-           "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one launch", "pairs": 10000,
+           "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one batch (both scheduler phases summed)", "pairs": 10000,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
            "tag": tag}
     if "SQ_INSTS_VALU" in vals:

@@ -278,6 +278,9 @@ constexpr int kSub = 8;
 #ifndef SLAM_WIN
 #define SLAM_WIN 4
 #endif
+#ifndef SLAM_SHIFT
+#define SLAM_SHIFT 1
+#endif
 #ifndef SLAM_HOIST
 #define SLAM_HOIST 0
 #endif
@@ -365,16 +368,36 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         for (int k = 0; k < QPT; ++k) nev += kWin * kSub * __popcll(__ballot(valid[k]));
     }
     lap(0);
-    // 2. clearance test: a query whose window is unchanged and whose carried
-    //    radius R (already reduced by this iteration's motion) satisfies
-    //    R^2 > M2 has every non-window candidate at d32 > M2: its window
-    //    result is the full screen's.  Only the other queries ("active") search
-    //    further; a group without active queries is done.
+    // 2. clearance test: the carried radius R (already reduced by this
+    //    iteration's motion) bounds every candidate outside the PREVIOUS window;
+    //    when the window moved by up to 2 sub-chunks, the sub-chunks that left it
+    //    are bounded by their boxes.  If the resulting radius Rl has Rl^2 > M2,
+    //    every non-window candidate has d32 > M2: the window result is the full
+    //    screen's.  Only the other queries ("active") search further; a group
+    //    without active queries is done.  Settled queries carry Rl with the new
+    //    window to the next iteration.
     bool act[QPT];
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-        const float R = st_radius(st[k]);
-        act[k] = valid[k] && !(ws[k] == st_ws(st[k]) && R * R * (1.0f - 1e-5f) > M2[k]);
+        const int wp = st_ws(st[k]);
+        const int sh = ws[k] - wp;
+        float rl = st_radius(st[k]);
+#if SLAM_SHIFT
+        if (sh != 0) {
+            const int c0 = sh > 0 ? wp : wp + kWin - 1;          // sub-chunks that left the window
+            const int c1 = sh > 0 ? wp + 1 : wp + kWin - 2;
+            const float4 b0 = box8[min(max(c0, 0), nsub - 1)];
+            const float4 b1 = box8[min(max(c1, 0), nsub - 1)];
+            float lb = box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, b0);
+            if (sh * sh > 1) lb = fminf(lb, box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, b1));
+            rl = fminf(rl, sqrtf(lb) * (1.0f - 1e-5f));
+        }
+        const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2[k];
+#else
+        const bool settled = sh == 0 && rl * rl * (1.0f - 1e-5f) > M2[k];
+#endif
+        act[k] = valid[k] && !settled;
+        if (settled && sh != 0) st[k] = st_pack(rl, ws[k]);
 #if SLAM_ABLATE & 1
         act[k] = false;
 #endif
@@ -416,13 +439,20 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
 #endif
         float gf = INFINITY, lmin = INFINITY;
+#if SLAM_ABLATE & 32
+        for (int w = 0; w < 0; ++w) {
+#else
         for (int w = 0; w < nw; ++w) {
+#endif
             const int sl = 64 * w + lane;
             // branch-free (no short-circuit): the LDS reads are not serialised behind exec-mask jumps
             const float glb = box_lb(f32x2{bx0, by0}, f32x2{bx1, by1}, box8[min(sl, nsub - 1)]);
             const bool gl = glb <= gM2;
             gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
             uint64_t live = __ballot((sl < nsub) & gl);
+#if SLAM_ABLATE & 16
+            live = 0;
+#endif
             if (stamping) tsub[3] += __popcll(live);
             while (live) {
                 // up to kBatch live sub-chunks per batch, straight-line: the box

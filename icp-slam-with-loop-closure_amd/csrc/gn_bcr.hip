@@ -27,6 +27,12 @@
 namespace slamhip {
 
 constexpr int kBcrThreads = 256;
+#ifndef SLAM_BCR_EVEN_FUSED
+#define SLAM_BCR_EVEN_FUSED 1   // even blocks: both operands staged at once, one fused k loop
+#endif
+#ifndef SLAM_BCR_ODD_REG
+#define SLAM_BCR_ODD_REG 1   // register-tiled odd-block elimination (0: LDS-blocked Cholesky + TRSM)
+#endif
 constexpr int kBcrMaxWb = 96;
 
 __host__ __device__ inline int64_t bcr_blk(int Wb) { return static_cast<int64_t>(Wb) * Wb; }
@@ -296,6 +302,122 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __re
     lap(3);
 }
 
+// Odd blocks, register-tiled variant (default): the Cholesky of D_i and the
+// forward substitution of its right-hand sides run as ONE unblocked
+// right-looking elimination of the augmented tile [D_i | R] held in registers —
+// 16 x 16 threads, thread (tr, tc) owns rows tr + 16u and columns tc + 16v of D_i
+// (T x T) and of R (T x (T+1)).  Pivot k: the owners of column k of D_i and
+// row k of R publish them in LDS (double-buffered, ONE barrier per pivot);
+// every thread scales them by 1/sqrt(piv) and applies the rank-1 update to its
+// entries with c > k (D_i) and r > k (R).  Column k of the registers becomes
+// L[:, k], row k of R becomes z_k: after Wb pivots the registers hold C_i and
+// C_i^-1 R.  Replaces bcr_chol + bcr_trsm (5 panel steps with 3 barriers each
+// and the LDS-resident tiles): C4 odd-kernel time per level 70 -> see DESIGN.
+template <int T>
+__global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* __restrict__ D,
+                                                                  const double* __restrict__ E,
+                                                                  double* __restrict__ Cs, double* __restrict__ Xs,
+                                                                  double* __restrict__ Ys, double* __restrict__ bz,
+                                                                  int32_t Wb, int32_t nb, int32_t s,
+                                                                  int32_t* __restrict__ status,
+                                                                  unsigned long long* __restrict__ stamps) {
+    constexpr int NW = T + 1;   // column tiles of R (part 1: Wb + 1 columns)
+    __shared__ double colb[2][16 * T];
+    __shared__ double rowb[2][16 * NW];
+    const bool stamping = stamps && blockIdx.x == 0 && blockIdx.y == 1 && threadIdx.x == 0;
+    unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
+    auto lap = [&](int q) {
+        if (stamping) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            stamps[q] += t1 - t0;
+            t0 = t1;
+        }
+    };
+    const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+    const int part = blockIdx.y;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const int64_t B2 = bcr_blk(Wb);
+    const double* Di = D + i * B2;
+    const double* Ep = E + p * B2;   // A[i, p]
+    const double* Ei = E + i * B2;   // A[n, i]; A[i, n] = its transpose
+    double a[T][T], r[T][NW];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+#pragma unroll
+        for (int v = 0; v < T; ++v) a[u][v] = Di[(tr + 16 * u) * Wb + tc + 16 * v];
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            const int R = tr + 16 * u, C = tc + 16 * w;
+            r[u][w] = part == 0 ? Ep[R * Wb + C] : (n < nb ? Ei[C * Wb + R] : 0.0);
+        }
+        r[u][T] = (part == 1 && tc == 0) ? bz[static_cast<int64_t>(i) * Wb + tr + 16 * u] : 0.0;
+    }
+    lap(0);
+    bool bad = false;
+#pragma unroll
+    for (int kv = 0; kv < T; ++kv) {
+        for (int kk = 0; kk < 16; ++kk) {
+            const int k = 16 * kv + kk, kb = k & 1;
+            if (tc == kk) {   // column k of D_i (all rows; rows < k are never read)
+#pragma unroll
+                for (int u = 0; u < T; ++u) colb[kb][tr + 16 * u] = a[u][kv];
+            }
+            if (tr == kk) {   // row k of R
+#pragma unroll
+                for (int w = 0; w < NW; ++w) rowb[kb][tc + 16 * w] = r[kv][w];
+            }
+            __syncthreads();
+            const double piv = colb[kb][k];
+            bad |= !(piv > 0.0);
+            const double rd = rsqrt(piv);   // reciprocal pivot: no fp64 division on the chain
+            const double dg = piv * rd;     // L[k][k]
+            double lr[T], lc[T], z[NW];
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                const int R = tr + 16 * u;
+                lr[u] = colb[kb][R] * rd;                    // L[R][k] for R > k
+                const int C = tc + 16 * u;
+                lc[u] = C > k ? colb[kb][C] * rd : 0.0;      // L[C][k], columns still to update
+            }
+#pragma unroll
+            for (int w = 0; w < NW; ++w) z[w] = rowb[kb][tc + 16 * w] * rd;   // z_k
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                const int R = tr + 16 * u;
+                const double l = R > k ? lr[u] : 0.0;
+#pragma unroll
+                for (int v = 0; v < T; ++v) a[u][v] = fma(-l, lc[v], a[u][v]);
+#pragma unroll
+                for (int w = 0; w < NW; ++w) r[u][w] = fma(-l, z[w], r[u][w]);
+                if (tc == kk) a[u][kv] = R > k ? lr[u] : (R == k ? dg : a[u][kv]);
+            }
+            if (tr == kk) {
+#pragma unroll
+                for (int w = 0; w < NW; ++w) r[kv][w] = z[w];
+            }
+        }
+    }
+    lap(1);
+    if (bad && part == 1 && tid == 0) *status = 1;
+    double* Out = (part == 0 ? Xs : Ys) + i * B2;
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const int R = tr + 16 * u;
+#pragma unroll
+        for (int w = 0; w < T; ++w) Out[R * Wb + tc + 16 * w] = r[u][w];
+        if (part == 1) {
+#pragma unroll
+            for (int v = 0; v < T; ++v) {
+                const int C = tc + 16 * v;
+                Cs[i * B2 + R * Wb + C] = C <= R ? a[u][v] : 0.0;
+            }
+            if (tc == 0) bz[static_cast<int64_t>(i) * Wb + R] = r[u][T];
+        }
+    }
+    lap(3);
+}
+
 // Even blocks of level s: Schur updates from the odd neighbours i1 = j - s
 // (its n is j) and i2 = j + s (its p is j), and the new coupling to j + 2s.
 // 16 x 16 threads, each a (Wb/16) x (Wb/16) register tile; the factors are
@@ -331,6 +453,64 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
             accE[u][v] = 0.0;
         }
     double bacc = 0.0;   // thread tid < Wb: row tid of the rhs update
+#if SLAM_BCR_EVEN_FUSED
+    // both operands staged at once, one barrier, one fused k loop:
+    //   part 0: L1 = Y1 (h1), L2 = X2 (h2): D_j -= Y1^T Y1 + X2^T X2, b_j -= Y1^T z1 + X2^T z2
+    //   part 1: L1 = X2, L2 = Y2:           E'_j = -Y2^T X2
+    {
+        const double* S1 = part == 0 ? (h1 ? Ys + i1 * B2 : nullptr) : Xs + i2 * B2;
+        const double* S2 = part == 0 ? (h2 ? Xs + i2 * B2 : nullptr) : Ys + i2 * B2;
+        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
+            int r, c;
+            bcr_rc(e, Wb, inv, r, c);
+            L1[r * ld + c] = S1 ? S1[e] : 0.0;
+            L2[r * ld + c] = S2 ? S2[e] : 0.0;
+        }
+        if (part == 0)
+            for (int r = tid; r < Wb; r += kBcrThreads) {
+                zv[r] = h1 ? bz[static_cast<int64_t>(i1) * Wb + r] : 0.0;
+                zv[Wb + r] = h2 ? bz[static_cast<int64_t>(i2) * Wb + r] : 0.0;
+            }
+        __syncthreads();
+        if (part == 0) {
+            for (int k = 0; k < Wb; ++k) {
+                double a1[T], b1[T], a2[T], b2[T];
+#pragma unroll
+                for (int u = 0; u < T; ++u) {
+                    a1[u] = L1[k * ld + tr + 16 * u];
+                    b1[u] = L1[k * ld + tc + 16 * u];
+                    a2[u] = L2[k * ld + tr + 16 * u];
+                    b2[u] = L2[k * ld + tc + 16 * u];
+                }
+#pragma unroll
+                for (int u = 0; u < T; ++u)
+#pragma unroll
+                    for (int v = 0; v < T; ++v) acc[u][v] = fma(a2[u], b2[v], fma(a1[u], b1[v], acc[u][v]));
+            }
+            if (tid < Wb) {
+                double b2acc = 0.0;
+                for (int k = 0; k < Wb; ++k) {
+                    bacc = fma(L1[k * ld + tid], zv[k], bacc);
+                    b2acc = fma(L2[k * ld + tid], zv[Wb + k], b2acc);
+                }
+                bacc += b2acc;
+            }
+        } else {
+            for (int k = 0; k < Wb; ++k) {
+                double y[T], b[T];
+#pragma unroll
+                for (int u = 0; u < T; ++u) {
+                    y[u] = L2[k * ld + tr + 16 * u];
+                    b[u] = L1[k * ld + tc + 16 * u];
+                }
+#pragma unroll
+                for (int u = 0; u < T; ++u)
+#pragma unroll
+                    for (int v = 0; v < T; ++v) accE[u][v] = fma(y[u], b[v], accE[u][v]);
+            }
+        }
+    }
+#else
     if (h1) {   // D_j -= Y1^T Y1, b_j -= Y1^T z1
         const double* Y1 = Ys + i1 * B2;
         for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
@@ -391,6 +571,7 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
         if (!hE && tid < Wb)
             for (int k = 0; k < Wb; ++k) bacc = fma(L1[k * ld + tid], zv[Wb + k], bacc);
     }
+#endif
     double* Dj = D + j * B2;
     double* Ej = E + j * B2;
 #pragma unroll
@@ -540,12 +721,19 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs, nv,
                        W, Wb, nb, D, E, bz);
     const size_t lds_odd = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + static_cast<size_t>(Wb) * (Wb + 2) + Wb);
+    (void)lds_odd;
     const size_t lds_even = sizeof(double) * (2 * static_cast<size_t>(Wb) * (Wb + 1) + 2 * static_cast<size_t>(Wb));
     const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 4 * static_cast<size_t>(Wb));
     using EvenFn = void (*)(double*, double*, const double*, const double*, double*, int32_t, int32_t, int32_t);
     static const EvenFn evens[6] = {bcr_even_kernel<1>, bcr_even_kernel<2>, bcr_even_kernel<3>,
                                     bcr_even_kernel<4>, bcr_even_kernel<5>, bcr_even_kernel<6>};
     const EvenFn even = evens[Wb / 16 - 1];
+    using OddFn = void (*)(const double*, const double*, double*, double*, double*, double*, int32_t, int32_t, int32_t,
+                           int32_t*, unsigned long long*);
+    static const OddFn odds[6] = {bcr_odd_reg_kernel<1>, bcr_odd_reg_kernel<2>, bcr_odd_reg_kernel<3>,
+                                  bcr_odd_reg_kernel<4>, bcr_odd_reg_kernel<5>, bcr_odd_reg_kernel<6>};
+    const OddFn odd = odds[Wb / 16 - 1];
+    (void)odd;
     // dynamic-LDS limits are raised once (not a stream operation: keeps the
     // launch sequence capturable into a hipGraph)
     static bool attrs = false;
@@ -562,8 +750,13 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     for (; s < nb; s *= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
+#if SLAM_BCR_ODD_REG
+        hipLaunchKernelGGL(odd, dim3(n_odd, 2), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
+                           stamps);
+#else
         hipLaunchKernelGGL(bcr_odd_kernel, dim3(n_odd, 2), dim3(kBcrThreads), lds_odd, st, D, E, Cs, Xs, Ys, bz, Wb,
                            nb, s, status, stamps);
+#endif
         hipLaunchKernelGGL(even, dim3(n_even, 2), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);

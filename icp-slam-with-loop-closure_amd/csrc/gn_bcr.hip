@@ -27,6 +27,9 @@
 namespace slamhip {
 
 constexpr int kBcrThreads = 256;
+#ifndef SLAM_BCR_BACK_TILED
+#define SLAM_BCR_BACK_TILED 1   // back-substitution mat-vecs: coalesced row segments + DPP row sums
+#endif
 #ifndef SLAM_BCR_EVEN_FUSED
 #define SLAM_BCR_EVEN_FUSED 1   // even blocks: both operands staged at once, one fused k loop
 #endif
@@ -632,6 +635,16 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_top_kernel(double* __restrict
 // Back-substitution of the odd blocks of level s: v = z - X x_p - Y x_n with
 // two threads per row (halves of k, x_p / x_n staged in LDS), then C^-T v by
 // one wave.
+// A double moved between lanes of a 16-lane row by DPP (both halves).
+template <int CTRL>
+__device__ __forceinline__ double dpp_row(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+template <int T>   // T = Wb / 16 (0: generic path)
 __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __restrict__ Cs,
                                                                const double* __restrict__ Xs,
                                                                const double* __restrict__ Ys,
@@ -660,6 +673,40 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
         xpn[Wb + k] = n < nb ? x[static_cast<int64_t>(n) * Wb + k] : 0.0;
     }
     __syncthreads();
+#if SLAM_BCR_BACK_TILED
+    if (T > 0) {
+        // 16 x 16 threads: thread (tr, tc) sums columns tc + 16 w of rows tr + 16 u
+        // (coalesced 128 B row segments straight from X_i, Y_i); the 16 lanes of a
+        // DPP row (tc = lane & 15) then add up with row butterflies
+        const int tr = tid >> 4, tc = tid & 15;
+        const double* X = Xs + i * B2;
+        const double* Y = Ys + i * B2;
+        double v[T];
+#pragma unroll
+        for (int u = 0; u < T; ++u) {
+            const int r = tr + 16 * u;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int w = 0; w < T; ++w) {
+                const int k = tc + 16 * w;
+                a0 = fma(X[r * Wb + k], xpn[k], a0);
+                a1 = fma(Y[r * Wb + k], xpn[Wb + k], a1);
+            }
+            v[u] = a0 + a1;
+        }
+#pragma unroll
+        for (int u = 0; u < T; ++u) {
+            v[u] += dpp_row<0xB1>(v[u]);    // quad_perm [1,0,3,2]
+            v[u] += dpp_row<0x4E>(v[u]);    // quad_perm [2,3,0,1]
+            v[u] += dpp_row<0x124>(v[u]);   // row_ror 4
+            v[u] += dpp_row<0x128>(v[u]);   // row_ror 8
+        }
+        if (tc == 0) {
+#pragma unroll
+            for (int u = 0; u < T; ++u) vv[tr + 16 * u] = bz[static_cast<int64_t>(i) * Wb + tr + 16 * u] - v[u];
+        }
+    } else
+#endif
     {
         const int r = tid >> 1, h = tid & 1;
         double v = 0.0;
@@ -733,15 +780,21 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     static const OddFn odds[6] = {bcr_odd_reg_kernel<1>, bcr_odd_reg_kernel<2>, bcr_odd_reg_kernel<3>,
                                   bcr_odd_reg_kernel<4>, bcr_odd_reg_kernel<5>, bcr_odd_reg_kernel<6>};
     const OddFn odd = odds[Wb / 16 - 1];
+    using BackFn = void (*)(const double*, const double*, const double*, const double*, double*, int32_t, int32_t,
+                            int32_t);
+    static const BackFn backs[6] = {bcr_back_kernel<1>, bcr_back_kernel<2>, bcr_back_kernel<3>,
+                                    bcr_back_kernel<4>, bcr_back_kernel<5>, bcr_back_kernel<6>};
+    const BackFn back = backs[Wb / 16 - 1];
     (void)odd;
     // dynamic-LDS limits are raised once (not a stream operation: keeps the
     // launch sequence capturable into a hipGraph)
     static bool attrs = false;
     if (!attrs) {
         const int lim = 160 * 1024;
-        const void* fns[] = {reinterpret_cast<const void*>(bcr_odd_kernel), reinterpret_cast<const void*>(bcr_back_kernel),
-                             reinterpret_cast<const void*>(bcr_top_kernel)};
+        const void* fns[] = {reinterpret_cast<const void*>(bcr_odd_kernel), reinterpret_cast<const void*>(bcr_top_kernel)};
         for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+        for (const BackFn f : backs)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim);
         for (const EvenFn f : evens)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim);
         attrs = true;
@@ -762,8 +815,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
     for (s /= 2; s >= 1; s /= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
-        hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(kBcrThreads), lds_back, st, Cs, Xs, Ys, bz, dx, Wb,
-                           nb, s);
+        hipLaunchKernelGGL(back, dim3(n_odd), dim3(kBcrThreads), lds_back, st, Cs, Xs, Ys, bz, dx, Wb, nb, s);
     }
     return check_launch("gn bcr kernels");
 }

@@ -45,7 +45,8 @@ __device__ __forceinline__ double wrap_pi(double a) {
 
 __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int32_t* __restrict__ ea,
                                     const int32_t* __restrict__ eb, const double* __restrict__ tf,
-                                    const double* __restrict__ w, int32_t E, double* __restrict__ contrib) {
+                                    const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
+                                    double* __restrict__ chi2e) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const int i = ea[e], j = eb[e];
@@ -98,6 +99,7 @@ __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int3
         o[30 + r] = we * gb;
     }
     o[33] = we * (ev[0] * ev[0] + ev[1] * ev[1] + ev[2] * ev[2]);
+    chi2e[e] = o[33];   // contiguous copy: the chi2 sum reads it coalesced
 }
 
 // Slot s: rows start at scalar r0 = slot_rc[2s], columns at c0 = slot_rc[2s+1].
@@ -478,15 +480,15 @@ __global__ void gn_update_kernel(double* __restrict__ poses, int32_t N, const in
 
 // chi2 = sum_e w_e |e_e|^2, deterministic single-block reduction (1024
 // threads, four independent partial sums per thread).
-__global__ __launch_bounds__(1024) void gn_chi2_kernel(const double* __restrict__ contrib, int32_t E,
+__global__ __launch_bounds__(1024) void gn_chi2_kernel(const double* __restrict__ chi2e, int32_t E,
                                                        double* __restrict__ out) {
     __shared__ double red[16];
     double q[4] = {0.0, 0.0, 0.0, 0.0};
     int e = threadIdx.x;
     for (; e + 3 * 1024 < E; e += 4 * 1024)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] += contrib[static_cast<int64_t>(e + u * 1024) * kGnContrib + 33];
-    for (; e < E; e += 1024) q[0] += contrib[static_cast<int64_t>(e) * kGnContrib + 33];
+        for (int u = 0; u < 4; ++u) q[u] += chi2e[e + u * 1024];
+    for (; e < E; e += 1024) q[0] += chi2e[e];
     double v[1] = {(q[0] + q[1]) + (q[2] + q[3])};
     block_sum<1, 16>(v, red);
     if (threadIdx.x == 0) *out = v[0];
@@ -537,7 +539,7 @@ int64_t slam_gn_work_size(int32_t N, int32_t E, int32_t W) {
     const int64_t steps = (nv + kGnS - 1) / kGnS;
     return static_cast<int64_t>(E) * kGnContrib + nv * (W + 1) + nv + MP * (MP + 1) +
            static_cast<int64_t>(kGnS) * lpw(W) + MP + steps * (kGnS + W) * kGnS + 8 +
-           bcr_work_size(static_cast<int32_t>(nv), W);
+           bcr_work_size(static_cast<int32_t>(nv), W) + E;   // last E: per-edge chi2 terms
 }
 
 int slam_gn_max_lds_band(void) {
@@ -563,10 +565,11 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
     double* Hb = contrib + static_cast<int64_t>(E) * kGnContrib;
     double* rhs = Hb + static_cast<int64_t>(nv) * (W + 1);
     double* gwin = rhs + nv;
+    double* chi2e = work + slam_gn_work_size(N, E, W) - E;
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, tf, w, E,
-                           contrib);
-    hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, contrib, E, out_chi2);
+                           contrib, chi2e);
+    hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, chi2e, E, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
     if (hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nv) * (W + 1), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");

@@ -36,3 +36,13 @@ print(f"extra sub-chunks visited per query group per iteration (wave 0): {t[4] /
 for n, v in zip(["  window scan", "  group box+mask", "  visits"], t[5:8]):
     print(f"{n:22s} {v / its:10.1f} ticks/iter")
 print(f"live sub-chunks per group per iteration: {t[8] / its / qpt:.2f}; test batches per group: {t[9] / its / qpt:.2f}")
+
+# wall time of the same launch without stamps, per iteration of pair 0
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+batch.launch()
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1)
+print(f"launch {ms:.3f} ms for {pairs} pairs (max iters {int(r.iters.max())}); pair 0: {its} iterations; "
+      f"stamp total {t[:4].sum() / its:.0f} ticks/iter; wall/iter of the longest pair {ms * 1e3 / r.iters.max():.1f} us")

@@ -305,6 +305,60 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __re
     lap(3);
 }
 
+// The augmented elimination of a register-tiled [D | R] (16 x 16 threads,
+// thread (tr, tc) owns rows tr + 16u, columns tc + 16v / tc + 16w): after it,
+// a holds the Cholesky factor C (lower; upper entries are garbage) and r holds
+// C^-1 R.  One barrier per pivot (double-buffered LDS broadcast of column k of
+// D and row k of R); rdg (optional, LDS) receives 1 / C[k][k].
+template <int T, int NW>
+__device__ __forceinline__ void bcr_reg_elim(double (&a)[T][T], double (&r)[T][NW], double (*colb)[16 * T],
+                                             double (*rowb)[16 * NW], int tr, int tc, bool& bad, double* rdg) {
+#pragma unroll
+    for (int kv = 0; kv < T; ++kv) {
+        for (int kk = 0; kk < 16; ++kk) {
+            const int k = 16 * kv + kk, kb = k & 1;
+            if (tc == kk) {   // column k of D_i (all rows; rows < k are never read)
+#pragma unroll
+                for (int u = 0; u < T; ++u) colb[kb][tr + 16 * u] = a[u][kv];
+            }
+            if (tr == kk) {   // row k of R
+#pragma unroll
+                for (int w = 0; w < NW; ++w) rowb[kb][tc + 16 * w] = r[kv][w];
+            }
+            __syncthreads();
+            const double piv = colb[kb][k];
+            bad |= !(piv > 0.0);
+            const double rd = rsqrt(piv);   // reciprocal pivot: no fp64 division on the chain
+            if (rdg && tr == kk && tc == kk) rdg[k] = rd;
+            const double dg = piv * rd;     // L[k][k]
+            double lr[T], lc[T], z[NW];
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                const int R = tr + 16 * u;
+                lr[u] = colb[kb][R] * rd;                    // L[R][k] for R > k
+                const int C = tc + 16 * u;
+                lc[u] = C > k ? colb[kb][C] * rd : 0.0;      // L[C][k], columns still to update
+            }
+#pragma unroll
+            for (int w = 0; w < NW; ++w) z[w] = rowb[kb][tc + 16 * w] * rd;   // z_k
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                const int R = tr + 16 * u;
+                const double l = R > k ? lr[u] : 0.0;
+#pragma unroll
+                for (int v = 0; v < T; ++v) a[u][v] = fma(-l, lc[v], a[u][v]);
+#pragma unroll
+                for (int w = 0; w < NW; ++w) r[u][w] = fma(-l, z[w], r[u][w]);
+                if (tc == kk) a[u][kv] = R > k ? lr[u] : (R == k ? dg : a[u][kv]);
+            }
+            if (tr == kk) {
+#pragma unroll
+                for (int w = 0; w < NW; ++w) r[kv][w] = z[w];
+            }
+        }
+    }
+}
+
 // Odd blocks, register-tiled variant (default): the Cholesky of D_i and the
 // forward substitution of its right-hand sides run as ONE unblocked
 // right-looking elimination of the augmented tile [D_i | R] held in registers —
@@ -358,49 +412,7 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
     }
     lap(0);
     bool bad = false;
-#pragma unroll
-    for (int kv = 0; kv < T; ++kv) {
-        for (int kk = 0; kk < 16; ++kk) {
-            const int k = 16 * kv + kk, kb = k & 1;
-            if (tc == kk) {   // column k of D_i (all rows; rows < k are never read)
-#pragma unroll
-                for (int u = 0; u < T; ++u) colb[kb][tr + 16 * u] = a[u][kv];
-            }
-            if (tr == kk) {   // row k of R
-#pragma unroll
-                for (int w = 0; w < NW; ++w) rowb[kb][tc + 16 * w] = r[kv][w];
-            }
-            __syncthreads();
-            const double piv = colb[kb][k];
-            bad |= !(piv > 0.0);
-            const double rd = rsqrt(piv);   // reciprocal pivot: no fp64 division on the chain
-            const double dg = piv * rd;     // L[k][k]
-            double lr[T], lc[T], z[NW];
-#pragma unroll
-            for (int u = 0; u < T; ++u) {
-                const int R = tr + 16 * u;
-                lr[u] = colb[kb][R] * rd;                    // L[R][k] for R > k
-                const int C = tc + 16 * u;
-                lc[u] = C > k ? colb[kb][C] * rd : 0.0;      // L[C][k], columns still to update
-            }
-#pragma unroll
-            for (int w = 0; w < NW; ++w) z[w] = rowb[kb][tc + 16 * w] * rd;   // z_k
-#pragma unroll
-            for (int u = 0; u < T; ++u) {
-                const int R = tr + 16 * u;
-                const double l = R > k ? lr[u] : 0.0;
-#pragma unroll
-                for (int v = 0; v < T; ++v) a[u][v] = fma(-l, lc[v], a[u][v]);
-#pragma unroll
-                for (int w = 0; w < NW; ++w) r[u][w] = fma(-l, z[w], r[u][w]);
-                if (tc == kk) a[u][kv] = R > k ? lr[u] : (R == k ? dg : a[u][kv]);
-            }
-            if (tr == kk) {
-#pragma unroll
-                for (int w = 0; w < NW; ++w) r[kv][w] = z[w];
-            }
-        }
-    }
+    bcr_reg_elim<T, NW>(a, r, colb, rowb, tr, tc, bad, nullptr);
     lap(1);
     if (bad && part == 1 && tid == 0) *status = 1;
     double* Out = (part == 0 ? Xs : Ys) + i * B2;
@@ -632,6 +644,50 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_top_kernel(double* __restrict
     }
 }
 
+// Last block, register-tiled: the elimination of [D_0 | b_0] (bcr_reg_elim with
+// one right-hand-side column), C_0 to LDS, then C_0^-T z by one wave.
+template <int T>
+__global__ __launch_bounds__(kBcrThreads) void bcr_top_reg_kernel(double* __restrict__ D,
+                                                                  const double* __restrict__ bz,
+                                                                  double* __restrict__ x, int32_t Wb,
+                                                                  int32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ double colb[2][16 * T];
+    __shared__ double rowb[2][16];
+    const int ldc = Wb + 1;
+    double* Cm = lds;
+    double* y = lds + static_cast<int64_t>(Wb) * ldc;
+    double* rdg = y + Wb;
+    const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+    double a[T][T], r[T][1];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+#pragma unroll
+        for (int v = 0; v < T; ++v) a[u][v] = D[(tr + 16 * u) * Wb + tc + 16 * v];
+        r[u][0] = tc == 0 ? bz[tr + 16 * u] : 0.0;
+    }
+    bool bad = false;
+    bcr_reg_elim<T, 1>(a, r, colb, rowb, tr, tc, bad, rdg);
+    if (bad && tid == 0) *status = 1;
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const int R = tr + 16 * u;
+#pragma unroll
+        for (int v = 0; v < T; ++v) {
+            const int C = tc + 16 * v;
+            if (C <= R) Cm[R * ldc + C] = a[u][v];
+        }
+        if (tc == 0) y[R] = r[u][0];
+    }
+    __syncthreads();
+    if (tid < 64) {
+        double v0 = tid < Wb ? y[tid] : 0.0, v1 = tid + 64 < Wb ? y[tid + 64] : 0.0;
+        bcr_backsub_wave(Cm, ldc, rdg, Wb, v0, v1);
+        if (tid < Wb) x[tid] = v0;
+        if (tid + 64 < Wb) x[tid + 64] = v1;
+    }
+}
+
 // Back-substitution of the odd blocks of level s: v = z - X x_p - Y x_n with
 // two threads per row (halves of k, x_p / x_n staged in LDS), then C^-T v by
 // one wave.
@@ -785,6 +841,11 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     static const BackFn backs[6] = {bcr_back_kernel<1>, bcr_back_kernel<2>, bcr_back_kernel<3>,
                                     bcr_back_kernel<4>, bcr_back_kernel<5>, bcr_back_kernel<6>};
     const BackFn back = backs[Wb / 16 - 1];
+    using TopFn = void (*)(double*, const double*, double*, int32_t, int32_t*);
+    static const TopFn tops[6] = {bcr_top_reg_kernel<1>, bcr_top_reg_kernel<2>, bcr_top_reg_kernel<3>,
+                                  bcr_top_reg_kernel<4>, bcr_top_reg_kernel<5>, bcr_top_reg_kernel<6>};
+    const TopFn top = tops[Wb / 16 - 1];
+    (void)top;
     (void)odd;
     // dynamic-LDS limits are raised once (not a stream operation: keeps the
     // launch sequence capturable into a hipGraph)
@@ -793,6 +854,9 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         const int lim = 160 * 1024;
         const void* fns[] = {reinterpret_cast<const void*>(bcr_odd_kernel), reinterpret_cast<const void*>(bcr_top_kernel)};
         for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+        for (const TopFn f : tops)   // these also hold 1.5 KB of static LDS
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      lim - 4096);
         for (const BackFn f : backs)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim);
         for (const EvenFn f : evens)
@@ -812,7 +876,11 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
 #endif
         hipLaunchKernelGGL(even, dim3(n_even, 2), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }
+#if SLAM_BCR_ODD_REG
+    hipLaunchKernelGGL(top, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
+#else
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
+#endif
     for (s /= 2; s >= 1; s /= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
         hipLaunchKernelGGL(back, dim3(n_odd), dim3(kBcrThreads), lds_back, st, Cs, Xs, Ys, bz, dx, Wb, nb, s);

@@ -162,6 +162,32 @@ def pgo_bench():
     return out
 
 
+def c1_bench(reps=20):
+    """Config C1 (BASELINE configs[0]): ONE drop-in ``src.icp.icp()`` call on a
+    1081-point pair (scripts/test_icp.py shape), host arrays in and out —
+    the latency an unchanged caller sees per call (upload, one B = 1 launch
+    with the transform history, download)."""
+    import torch
+    import src.icp as icp
+    from slamhip import se2, synthetic
+    seq = synthetic.make_sequence(2, seed=0)
+    pc1 = np.c_[seq.scans[1], np.ones(len(seq.scans[1]))]
+    pc2 = np.c_[seq.scans[0], np.ones(len(seq.scans[0]))]
+    init = se2.pose_to_mat(seq.odometry[1] - seq.odometry[0])
+    tfs, _ = icp.icp(pc1, pc2, init_transform=init.copy(), epsilon=0.05, max_iters=100)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        tfs, _ = icp.icp(pc1, pc2, init_transform=init.copy(), epsilon=0.05, max_iters=100)
+        ts.append(time.perf_counter() - t0)
+    its = len(tfs) - 1
+    return {"c1_icp_call_ms": round(float(np.median(ts)) * 1e3, 3), "c1_iterations": its,
+            "c1_ref_cpu_s_per_call_est": round(0.0318 * its, 3),
+            "c1_note": "median of %d drop-in src.icp.icp() calls, host arrays in/out; reference CPU estimate = "
+                       "31.8 ms per get_correspondences at 1081^2 (SURVEY.md section 8(a) a2) x iterations" % reps}
+
+
 def main():
     args = parse()
     import torch
@@ -336,6 +362,10 @@ def main():
             out["pgo"] = pgo_bench()
         except Exception as e:
             out["pgo"] = {"error": repr(e)}
+        try:
+            out["c1"] = c1_bench()
+        except Exception as e:
+            out["c1"] = {"error": repr(e)}
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

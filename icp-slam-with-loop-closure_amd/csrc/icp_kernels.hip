@@ -1134,6 +1134,12 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
+#ifndef SLAM_SCHED_NMID
+#define SLAM_SCHED_NMID 0   // capped middle phases between the probe and the final phase (A/B)
+#endif
+#ifndef SLAM_SCHED_MID
+#define SLAM_SCHED_MID 12
+#endif
 #ifndef SLAM_SCHED_KEY
 #define SLAM_SCHED_KEY 0   // 0: last error change, 1: error level (A/B)
 #endif
@@ -1190,21 +1196,21 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     a.phase_cap = probe;
     a.sched_key = key;
     int rc = launch(false, a, B, max_n1, max_n2, stream);
-    if (rc == 0) {
-        const int g = (B + 255) / 256;
+    const int g = (B + 255) / 256;
 #if SLAM_SCHED_KEY == 1
-        const float thr = 1.0f;
+    const float thr = 1.0f;
 #else
-        const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
+    const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
 #endif
+    // optional capped middle phases (A/B: SLAM_SCHED_MID iterations each), then the rest
+    for (int ph = 0; rc == 0 && ph <= SLAM_SCHED_NMID; ++ph) {
         (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
         hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
         hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);
         hipLaunchKernelGGL(sched_scatter_kernel, dim3(g), dim3(256), 0, s, bucket, B, hist, order);
         rc = check_launch("icp scheduler kernels");
-    }
-    if (rc == 0) {
-        a.phase_cap = 0;
+        if (rc != 0) break;
+        a.phase_cap = ph < SLAM_SCHED_NMID ? SLAM_SCHED_MID : 0;
         a.resume = 1;
         a.order = order;
         rc = launch(false, a, B, max_n1, max_n2, stream);

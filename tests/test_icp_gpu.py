@@ -340,3 +340,22 @@ def test_schedule_is_invisible(k):
             assert np.array_equal(h0, h1)
     assert np.array_equal(outs[-1].tf, ref_ro.tf) and np.array_equal(outs[-1].iters, ref_ro.iters)
     assert np.array_equal(outs[-1].err, ref_ro.err)
+
+
+def test_default_schedule_large_batch(k):
+    """A batch above the scheduler threshold (2,100 pairs) through the default
+    two-phase path equals the single launch bit for bit."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 2100
+    seq, inits = _sequence_pairs(n, seed=21, n_beams=181)
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    phased = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
+    try:
+        assert lib.slam_icp_set_schedule(0, 2048) == 0
+        single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
+    finally:
+        lib.slam_icp_set_schedule(5, 2048)
+    assert phased.iters.max() > 5
+    assert np.array_equal(phased.iters, single.iters)
+    assert np.array_equal(phased.tf, single.tf) and np.array_equal(phased.err, single.err)

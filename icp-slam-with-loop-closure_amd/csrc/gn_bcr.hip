@@ -27,15 +27,6 @@
 namespace slamhip {
 
 constexpr int kBcrThreads = 256;
-#ifndef SLAM_BCR_BACK_TILED
-#define SLAM_BCR_BACK_TILED 1   // back-substitution mat-vecs: coalesced row segments + DPP row sums
-#endif
-#ifndef SLAM_BCR_EVEN_FUSED
-#define SLAM_BCR_EVEN_FUSED 1   // even blocks: both operands staged at once, one fused k loop
-#endif
-#ifndef SLAM_BCR_ODD_REG
-#define SLAM_BCR_ODD_REG 1   // register-tiled odd-block elimination (0: LDS-blocked Cholesky + TRSM)
-#endif
 constexpr int kBcrMaxWb = 96;
 
 __host__ __device__ inline int64_t bcr_blk(int Wb) { return static_cast<int64_t>(Wb) * Wb; }
@@ -71,238 +62,6 @@ __global__ void bcr_load_kernel(const double* __restrict__ Hb, const double* __r
         E[idx] = (R2 < nv && d2 <= W) ? Hb[R2 * ld + d2] : 0.0;
     }
     if (c == 0) bz[static_cast<int64_t>(i) * Wb + r] = R < nv ? rhs[R] : 0.0;
-}
-
-// ---- blocked dense kernels on a Wb x Wb LDS tile (Wb a multiple of 16) -------
-// Every loop below has compile-time trip counts inside a 16-wide block, so the
-// LDS reads of a block issue back to back instead of one latency per FMA.
-
-// Wave 0, lanes 0..15: factor the 16 x 16 diagonal block at k0 in registers
-// (lane i holds row i; pivots and L[c][j] broadcast with v_readlane).
-__device__ inline bool bcr_diag16(double* Cm, int ldc, int k0, double* rdg) {
-    const int lane = threadIdx.x & 63;
-    double row[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) row[c] = (lane < 16 && c <= lane) ? Cm[(k0 + lane) * ldc + k0 + c] : 0.0;
-    bool bad = false;
-    double rdl = 0.0;   // lane j: 1 / L[j][j]
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const double piv = readlane_d(row[j], j);
-        bad |= !(piv > 0.0);
-        const double rd = rsqrt(piv);   // reciprocal pivots: no fp64 division on the chain
-        const double d = piv * rd;
-        if (lane == j) {
-            row[j] = d;
-            rdl = rd;
-        }
-        if (lane > j) row[j] = row[j] * rd;
-#pragma unroll
-        for (int c = j + 1; c < 16; ++c) {
-            const double lcj = readlane_d(row[j], c);
-            if (lane >= c) row[c] = fma(-row[j], lcj, row[c]);
-        }
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c)
-            if (c <= lane) Cm[(k0 + lane) * ldc + k0 + c] = row[c];
-        rdg[k0 + lane] = rdl;
-    }
-    return bad;
-}
-
-// Blocked right-looking Cholesky of the LDS tile (lower triangle), all
-// threads; returns through *status on a non-positive pivot.
-__device__ inline void bcr_chol(double* Cm, int ldc, double* rdg, int Wb, int32_t* status) {
-    const int tid = threadIdx.x;
-    for (int k0 = 0; k0 < Wb; k0 += 16) {
-        if (tid < 64) {
-            const bool bad = bcr_diag16(Cm, ldc, k0, rdg);
-            if (bad && tid == 0 && status) *status = 1;
-        }
-        __syncthreads();
-        const int r0 = k0 + 16, n = Wb - r0;
-        // panel: L[r][k0+t] = (A[r][k0+t] - sum_q L[r][k0+q] L[k0+t][k0+q]) / L[k0+t][k0+t]
-        for (int i = tid; i < n; i += kBcrThreads) {
-            asm volatile("" ::: "memory");   // keep the L_KK reads in the loop (no hoisting into 272 VGPRs)
-            const int r = r0 + i;
-            double l[16];
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                asm volatile("" ::: "memory");
-                double v = Cm[r * ldc + k0 + t];
-#pragma unroll
-                for (int q = 0; q < t; ++q) v = fma(-l[q], Cm[(k0 + t) * ldc + k0 + q], v);
-                l[t] = v * rdg[k0 + t];
-            }
-#pragma unroll
-            for (int t = 0; t < 16; ++t) Cm[r * ldc + k0 + t] = l[t];
-        }
-        __syncthreads();
-        // trailing update of the lower triangle, 4 x 4 register tiles
-        const int nt = n >> 2;
-        for (int q = tid; q < nt * (nt + 1) / 2; q += kBcrThreads) {
-            asm volatile("" ::: "memory");
-            int ti = static_cast<int>((sqrtf(8.0f * q + 1.0f) - 1.0f) * 0.5f);
-            while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
-            while (ti * (ti + 1) / 2 > q) --ti;
-            const int tj = q - ti * (ti + 1) / 2;
-            double acc[4][4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
-#pragma unroll 4
-            for (int t = 0; t < 16; ++t) {
-                double a[4], b[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    a[u] = Cm[(r0 + 4 * ti + u) * ldc + k0 + t];
-                    b[u] = Cm[(r0 + 4 * tj + u) * ldc + k0 + t];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int r = r0 + 4 * ti + u, c = r0 + 4 * tj + v;
-                    if (c <= r) Cm[r * ldc + c] -= acc[u][v];
-                }
-        }
-        __syncthreads();
-    }
-}
-
-// Blocked forward substitution C X = R in place for nc columns of R (LDS,
-// row stride ldr), all threads.
-__device__ inline void bcr_trsm(const double* Cm, int ldc, const double* rdg, double* Rm, int ldr, int Wb, int nc) {
-    const int tid = threadIdx.x;
-    for (int k0 = 0; k0 < Wb; k0 += 16) {
-        // diagonal block: one thread per column
-        for (int c = tid; c < nc; c += kBcrThreads) {
-            asm volatile("" ::: "memory");   // keep the L_KK reads in the loop
-            double x[16];
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                asm volatile("" ::: "memory");   // row t's reads stay in step t (bounded live registers)
-                double v = Rm[(k0 + t) * ldr + c];
-#pragma unroll
-                for (int q = 0; q < t; ++q) v = fma(-Cm[(k0 + t) * ldc + k0 + q], x[q], v);
-                x[t] = v * rdg[k0 + t];
-            }
-#pragma unroll
-            for (int t = 0; t < 16; ++t) Rm[(k0 + t) * ldr + c] = x[t];
-        }
-        __syncthreads();
-        // rows below: R[r][c] -= sum_t L[r][k0+t] X[k0+t][c], 4 x 4 tiles
-        const int r0 = k0 + 16, nr = (Wb - r0) >> 2, ncl = (nc + 3) >> 2;
-        for (int q = tid; q < nr * ncl; q += kBcrThreads) {
-            asm volatile("" ::: "memory");
-            const int ti = q / ncl, tj = q % ncl;
-            double acc[4][4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
-#pragma unroll 4
-            for (int t = 0; t < 16; ++t) {
-                double a[4], b[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    a[u] = Cm[(r0 + 4 * ti + u) * ldc + k0 + t];
-                    const int c = 4 * tj + u;
-                    b[u] = c < nc ? Rm[(k0 + t) * ldr + c] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int c = 4 * tj + v;
-                    if (c < nc) Rm[(r0 + 4 * ti + u) * ldr + c] -= acc[u][v];
-                }
-        }
-        __syncthreads();
-    }
-}
-
-// Odd blocks of level s, two workgroups per block (blockIdx.y): both factor
-// C_i (cheap next to the solves); part 0 solves X = C^-1 E_p, part 1 solves
-// [Y | z] = C^-1 [E_i^T | b_i] and stores C_i (into Cs, never over D: the
-// other part may still be reading D_i).
-__global__ __launch_bounds__(kBcrThreads) void bcr_odd_kernel(const double* __restrict__ D,
-                                                              const double* __restrict__ E, double* __restrict__ Cs,
-                                                              double* __restrict__ Xs, double* __restrict__ Ys,
-                                                              double* __restrict__ bz, int32_t Wb, int32_t nb,
-                                                              int32_t s, int32_t* __restrict__ status,
-                                                              unsigned long long* __restrict__ stamps) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int ldc = Wb + 1, ldr = Wb + 2;
-    // diagnostics: phase s_memtime of workgroup (0, 1), accumulated over levels
-    const bool stamping = stamps && blockIdx.x == 0 && blockIdx.y == 1 && threadIdx.x == 0;
-    unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
-    auto lap = [&](int q) {
-        if (stamping) {
-            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-            stamps[q] += t1 - t0;
-            t0 = t1;
-        }
-    };
-    double* Cm = lds;                                   // [Wb][Wb + 1]
-    double* Rm = lds + static_cast<int64_t>(Wb) * ldc;  // [Wb][Wb + 2]
-    double* rdg = Rm + static_cast<int64_t>(Wb) * ldr;  // [Wb] reciprocal diagonal of C
-    const int tid = threadIdx.x;
-    const int part = blockIdx.y;
-    const int i = s + 2 * s * blockIdx.x;
-    const int p = i - s, n = i + s;
-    const int64_t B2 = bcr_blk(Wb);
-    const double* Di = D + i * B2;
-    const double* Ep = E + p * B2;                      // A[i, p]: rows of i, columns of p
-    const double* Ei = E + i * B2;                      // A[n, i]; A[i, n] = its transpose
-    const float inv = 1.0f / static_cast<float>(Wb);
-    for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-        int r, c;
-        bcr_rc(e, Wb, inv, r, c);
-        Cm[r * ldc + c] = Di[e];
-        if (part == 0) Rm[r * ldr + c] = Ep[e];
-        else Rm[r * ldr + c] = n < nb ? Ei[c * Wb + r] : 0.0;
-    }
-    if (part == 1)
-        for (int r = tid; r < Wb; r += kBcrThreads) Rm[r * ldr + Wb] = bz[static_cast<int64_t>(i) * Wb + r];
-    __syncthreads();
-    lap(0);
-    bcr_chol(Cm, ldc, rdg, Wb, part == 1 ? status : nullptr);
-    lap(1);
-    bcr_trsm(Cm, ldc, rdg, Rm, ldr, Wb, part == 0 ? Wb : Wb + 1);
-    lap(2);
-    if (part == 0) {
-        double* Xi = Xs + i * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            int r, c;
-            bcr_rc(e, Wb, inv, r, c);
-            Xi[e] = Rm[r * ldr + c];
-        }
-    } else {
-        double* Yi = Ys + i * B2;
-        double* Ci = Cs + i * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            int r, c;
-            bcr_rc(e, Wb, inv, r, c);
-            Yi[e] = Rm[r * ldr + c];
-            Ci[e] = c <= r ? Cm[r * ldc + c] : 0.0;
-        }
-        for (int r = tid; r < Wb; r += kBcrThreads) bz[static_cast<int64_t>(i) * Wb + r] = Rm[r * ldr + Wb];
-    }
-    lap(3);
 }
 
 // The augmented elimination of a register-tiled [D | R] (16 x 16 threads,
@@ -359,7 +118,7 @@ __device__ __forceinline__ void bcr_reg_elim(double (&a)[T][T], double (&r)[T][N
     }
 }
 
-// Odd blocks, register-tiled variant (default): the Cholesky of D_i and the
+// Odd blocks: the Cholesky of D_i and the
 // forward substitution of its right-hand sides run as ONE unblocked
 // right-looking elimination of the augmented tile [D_i | R] held in registers —
 // 16 x 16 threads, thread (tr, tc) owns rows tr + 16u and columns tc + 16v of D_i
@@ -368,8 +127,8 @@ __device__ __forceinline__ void bcr_reg_elim(double (&a)[T][T], double (&r)[T][N
 // every thread scales them by 1/sqrt(piv) and applies the rank-1 update to its
 // entries with c > k (D_i) and r > k (R).  Column k of the registers becomes
 // L[:, k], row k of R becomes z_k: after Wb pivots the registers hold C_i and
-// C_i^-1 R.  Replaces bcr_chol + bcr_trsm (5 panel steps with 3 barriers each
-// and the LDS-resident tiles): C4 odd-kernel time per level 70 -> see DESIGN.
+// C_i^-1 R.  (It replaced an LDS-blocked Cholesky + TRSM with 3 barriers per
+// 16-column panel: 57 -> 46 us per C4 level)
 template <int T>
 __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* __restrict__ D,
                                                                   const double* __restrict__ E,
@@ -468,7 +227,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
             accE[u][v] = 0.0;
         }
     double bacc = 0.0;   // thread tid < Wb: row tid of the rhs update
-#if SLAM_BCR_EVEN_FUSED
     // both operands staged at once, one barrier, one fused k loop:
     //   part 0: L1 = Y1 (h1), L2 = X2 (h2): D_j -= Y1^T Y1 + X2^T X2, b_j -= Y1^T z1 + X2^T z2
     //   part 1: L1 = X2, L2 = Y2:           E'_j = -Y2^T X2
@@ -525,68 +283,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
             }
         }
     }
-#else
-    if (h1) {   // D_j -= Y1^T Y1, b_j -= Y1^T z1
-        const double* Y1 = Ys + i1 * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            int r, c;
-            bcr_rc(e, Wb, inv, r, c);
-            L1[r * ld + c] = Y1[e];
-        }
-        for (int r = tid; r < Wb; r += kBcrThreads) zv[r] = bz[static_cast<int64_t>(i1) * Wb + r];
-        __syncthreads();
-        for (int k = 0; k < Wb; ++k) {
-            double a[T], b[T];
-#pragma unroll
-            for (int u = 0; u < T; ++u) {
-                a[u] = u < nt ? L1[k * ld + tr + 16 * u] : 0.0;
-                b[u] = u < nt ? L1[k * ld + tc + 16 * u] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < T; ++u)
-#pragma unroll
-                for (int v = 0; v < T; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
-        }
-        if (tid < Wb)
-            for (int k = 0; k < Wb; ++k) bacc = fma(L1[k * ld + tid], zv[k], bacc);
-        __syncthreads();
-    }
-    if (h2) {   // D_j -= X2^T X2, b_j -= X2^T z2, E'_j = -Y2^T X2
-        const double* X2 = Xs + i2 * B2;
-        const double* Y2 = Ys + i2 * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            int r, c;
-            bcr_rc(e, Wb, inv, r, c);
-            L1[r * ld + c] = X2[e];
-            if (hE) L2[r * ld + c] = Y2[e];
-        }
-        // part 1 only needs Y2^T X2; part 0 only X2^T X2
-        for (int r = tid; r < Wb; r += kBcrThreads) zv[Wb + r] = bz[static_cast<int64_t>(i2) * Wb + r];
-        __syncthreads();
-        for (int k = 0; k < Wb; ++k) {
-            double a[T], b[T], y[T];
-#pragma unroll
-            for (int u = 0; u < T; ++u) {
-                a[u] = u < nt ? L1[k * ld + tr + 16 * u] : 0.0;
-                b[u] = u < nt ? L1[k * ld + tc + 16 * u] : 0.0;
-                y[u] = (hE && u < nt) ? L2[k * ld + tr + 16 * u] : 0.0;
-            }
-            if (hE) {
-#pragma unroll
-                for (int u = 0; u < T; ++u)
-#pragma unroll
-                    for (int v = 0; v < T; ++v) accE[u][v] = fma(y[u], b[v], accE[u][v]);
-            } else {
-#pragma unroll
-                for (int u = 0; u < T; ++u)
-#pragma unroll
-                    for (int v = 0; v < T; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
-            }
-        }
-        if (!hE && tid < Wb)
-            for (int k = 0; k < Wb; ++k) bacc = fma(L1[k * ld + tid], zv[Wb + k], bacc);
-    }
-#endif
     double* Dj = D + j * B2;
     double* Ej = E + j * B2;
 #pragma unroll
@@ -613,34 +309,6 @@ __device__ inline void bcr_backsub_wave(const double* Cm, int ldc, const double*
         if (lane + 64 == k) v1 = xk;
         if (lane < k) v0 = fma(-Cm[k * ldc + lane], xk, v0);
         if (lane + 64 < k) v1 = fma(-Cm[k * ldc + lane + 64], xk, v1);
-    }
-}
-
-// Last block (index 0): Cholesky and both substitutions -> x_0.
-__global__ __launch_bounds__(kBcrThreads) void bcr_top_kernel(double* __restrict__ D, const double* __restrict__ bz,
-                                                              double* __restrict__ x, int32_t Wb,
-                                                              int32_t* __restrict__ status) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int ldc = Wb + 1;
-    double* Cm = lds;
-    double* y = lds + static_cast<int64_t>(Wb) * ldc;
-    double* rdg = y + Wb;
-    const int tid = threadIdx.x;
-    const float inv = 1.0f / static_cast<float>(Wb);
-    for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-        int r, c;
-        bcr_rc(e, Wb, inv, r, c);
-        Cm[r * ldc + c] = D[e];
-    }
-    for (int r = tid; r < Wb; r += kBcrThreads) y[r] = bz[r];
-    __syncthreads();
-    bcr_chol(Cm, ldc, rdg, Wb, status);
-    bcr_trsm(Cm, ldc, rdg, y, 1, Wb, 1);
-    if (tid < 64) {
-        double v0 = tid < Wb ? y[tid] : 0.0, v1 = tid + 64 < Wb ? y[tid + 64] : 0.0;
-        bcr_backsub_wave(Cm, ldc, rdg, Wb, v0, v1);
-        if (tid < Wb) x[tid] = v0;
-        if (tid + 64 < Wb) x[tid + 64] = v1;
     }
 }
 
@@ -688,9 +356,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_top_reg_kernel(double* __rest
     }
 }
 
-// Back-substitution of the odd blocks of level s: v = z - X x_p - Y x_n with
-// two threads per row (halves of k, x_p / x_n staged in LDS), then C^-T v by
-// one wave.
 // A double moved between lanes of a 16-lane row by DPP (both halves).
 template <int CTRL>
 __device__ __forceinline__ double dpp_row(double v) {
@@ -700,7 +365,10 @@ __device__ __forceinline__ double dpp_row(double v) {
     return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
-template <int T>   // T = Wb / 16 (0: generic path)
+// Back-substitution of the odd blocks of level s: v = z - X x_p - Y x_n
+// (x_p / x_n staged in LDS, X / Y read in 128 B row segments, DPP row sums),
+// then C^-T v by one wave.
+template <int T>   // T = Wb / 16
 __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __restrict__ Cs,
                                                                const double* __restrict__ Xs,
                                                                const double* __restrict__ Ys,
@@ -729,8 +397,7 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
         xpn[Wb + k] = n < nb ? x[static_cast<int64_t>(n) * Wb + k] : 0.0;
     }
     __syncthreads();
-#if SLAM_BCR_BACK_TILED
-    if (T > 0) {
+    {
         // 16 x 16 threads: thread (tr, tc) sums columns tc + 16 w of rows tr + 16 u
         // (coalesced 128 B row segments straight from X_i, Y_i); the 16 lanes of a
         // DPP row (tc = lane & 15) then add up with row butterflies
@@ -761,25 +428,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
 #pragma unroll
             for (int u = 0; u < T; ++u) vv[tr + 16 * u] = bz[static_cast<int64_t>(i) * Wb + tr + 16 * u] - v[u];
         }
-    } else
-#endif
-    {
-        const int r = tid >> 1, h = tid & 1;
-        double v = 0.0;
-        if (r < Wb) {
-            const double* X = Xs + i * B2 + static_cast<int64_t>(r) * Wb;
-            const double* Y = Ys + i * B2 + static_cast<int64_t>(r) * Wb;
-            const int k0 = h * (Wb >> 1), k1 = k0 + (Wb >> 1);
-            double v1 = 0.0;
-#pragma unroll 8
-            for (int k = k0; k < k1; ++k) {
-                v = fma(X[k], xpn[k], v);
-                v1 = fma(Y[k], xpn[Wb + k], v1);
-            }
-            v += v1;
-        }
-        v += __shfl_xor(v, 1, 64);
-        if (r < Wb && h == 0) vv[r] = bz[static_cast<int64_t>(i) * Wb + r] - v;
     }
     __syncthreads();
     if (tid < 64) {
@@ -823,8 +471,6 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     const int64_t tot = nb * B2;
     hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs, nv,
                        W, Wb, nb, D, E, bz);
-    const size_t lds_odd = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + static_cast<size_t>(Wb) * (Wb + 2) + Wb);
-    (void)lds_odd;
     const size_t lds_even = sizeof(double) * (2 * static_cast<size_t>(Wb) * (Wb + 1) + 2 * static_cast<size_t>(Wb));
     const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 4 * static_cast<size_t>(Wb));
     using EvenFn = void (*)(double*, double*, const double*, const double*, double*, int32_t, int32_t, int32_t);
@@ -845,15 +491,11 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     static const TopFn tops[6] = {bcr_top_reg_kernel<1>, bcr_top_reg_kernel<2>, bcr_top_reg_kernel<3>,
                                   bcr_top_reg_kernel<4>, bcr_top_reg_kernel<5>, bcr_top_reg_kernel<6>};
     const TopFn top = tops[Wb / 16 - 1];
-    (void)top;
-    (void)odd;
     // dynamic-LDS limits are raised once (not a stream operation: keeps the
     // launch sequence capturable into a hipGraph)
     static bool attrs = false;
     if (!attrs) {
         const int lim = 160 * 1024;
-        const void* fns[] = {reinterpret_cast<const void*>(bcr_odd_kernel), reinterpret_cast<const void*>(bcr_top_kernel)};
-        for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
         for (const TopFn f : tops)   // these also hold 1.5 KB of static LDS
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       lim - 4096);
@@ -867,20 +509,11 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     for (; s < nb; s *= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
-#if SLAM_BCR_ODD_REG
         hipLaunchKernelGGL(odd, dim3(n_odd, 2), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
                            stamps);
-#else
-        hipLaunchKernelGGL(bcr_odd_kernel, dim3(n_odd, 2), dim3(kBcrThreads), lds_odd, st, D, E, Cs, Xs, Ys, bz, Wb,
-                           nb, s, status, stamps);
-#endif
         hipLaunchKernelGGL(even, dim3(n_even, 2), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }
-#if SLAM_BCR_ODD_REG
     hipLaunchKernelGGL(top, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
-#else
-    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
-#endif
     for (s /= 2; s >= 1; s /= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
         hipLaunchKernelGGL(back, dim3(n_odd), dim3(kBcrThreads), lds_back, st, Cs, Xs, Ys, bz, dx, Wb, nb, s);

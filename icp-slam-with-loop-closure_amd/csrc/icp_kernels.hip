@@ -281,9 +281,6 @@ constexpr int kSub = 8;
 #ifndef SLAM_SHIFT
 #define SLAM_SHIFT 1
 #endif
-#ifndef SLAM_HOIST
-#define SLAM_HOIST 0
-#endif
 #ifndef SLAM_ABLATE
 #define SLAM_ABLATE 0   // diagnostics only (tools/ab_fixed.py): 1 no visits, 2 no certification, 4 no block sums, 8 no clearance
 #endif
@@ -414,30 +411,14 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     //    (non-live sub-chunks: gf; live sub-chunks outside the window: lmin)
     //    is the new clearance radius.
     const int nw = (nsub + 63) >> 6;
-#if SLAM_HOIST
-    // boxes of every group at once: independent reduction chains interleave
-    float hb[QPT][5];
-#pragma unroll
-    for (int k = 0; k < QPT; ++k) {
-        hb[k][0] = wave_min_f(act[k] ? qx[k] : INFINITY);
-        hb[k][1] = wave_max_f(act[k] ? qx[k] : -INFINITY);
-        hb[k][2] = wave_min_f(act[k] ? qy[k] : INFINITY);
-        hb[k][3] = wave_max_f(act[k] ? qy[k] : -INFINITY);
-        hb[k][4] = wave_max_f(act[k] ? M2[k] : -INFINITY);
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
         if (__ballot(act[k]) == 0) continue;   // wave-uniform
-#if SLAM_HOIST
-        const float bx0 = hb[k][0], bx1 = hb[k][1], by0 = hb[k][2], by1 = hb[k][3], gM2 = hb[k][4];
-#else
         const float bx0 = wave_min_f(act[k] ? qx[k] : INFINITY);
         const float bx1 = wave_max_f(act[k] ? qx[k] : -INFINITY);
         const float by0 = wave_min_f(act[k] ? qy[k] : INFINITY);
         const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
         const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
-#endif
         float gf = INFINITY, lmin = INFINITY;
 #if SLAM_ABLATE & 32
         for (int w = 0; w < 0; ++w) {

@@ -133,6 +133,25 @@ __device__ __forceinline__ float screen_d32(float px, float py, float qx, float 
     return fmaf(dy, dy, dx * dx);
 }
 
+// fp32 candidates are stored as pairs (x_2p, x_2p+1, y_2p, y_2p+1): one float4
+// read gives two candidates whose distances to a query are three packed ops
+// (v_pk_add x2, v_pk_mul, v_pk_fma) — per element exactly screen_d32.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 cf_at(const float2* candf, int j) {
+    const float* f = reinterpret_cast<const float*>(candf) + 4 * (j >> 1) + (j & 1);
+    return make_float2(f[0], f[2]);
+}
+__device__ __forceinline__ void cf_put(float2* candf, int j, float x, float y) {
+    float* f = reinterpret_cast<float*>(candf) + 4 * (j >> 1) + (j & 1);
+    f[0] = x;
+    f[2] = y;
+}
+__device__ __forceinline__ f32x2v screen_pair(const float4& p, float qx, float qy) {
+    const f32x2v dx = f32x2v{p.x, p.y} - qx;
+    const f32x2v dy = f32x2v{p.z, p.w} - qy;
+    return __builtin_elementwise_fma(dy, dy, dx * dx);
+}
+
 template <int QPT>
 __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf, int n_pad,
                                                 const float (&qx)[QPT], const float (&qy)[QPT],
@@ -143,7 +162,7 @@ __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf
         for (int k = 0; k < QPT; ++k) cm[k] = INFINITY;
 #pragma unroll 4
         for (int j = c0; j < c0 + kChunk; ++j) {
-            const float2 p = candf[j];
+            const float2 p = cf_at(candf, j);
 #pragma unroll
             for (int k = 0; k < QPT; ++k) cm[k] = fminf(cm[k], screen_d32(p.x, p.y, qx[k], qy[k]));
         }
@@ -221,29 +240,6 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
 }
 #undef SLAM_DPP
 
-// Chunk-minimum update of (M1, M2, C1) with the minimum cm of chunk c.
-__device__ __forceinline__ void take_chunk(float cm, int c, float& M1, float& M2, int& C1) {
-    const bool lt = cm < M1;
-    M2 = __builtin_amdgcn_fmed3f(M1, M2, cm);
-    C1 = lt ? c * kChunk : C1;
-    M1 = fminf(M1, cm);
-}
-
-// Full scan of chunk c for one query per lane.
-__device__ __forceinline__ void scan_chunk(const float2* __restrict__ candf, int c, float qx, float qy,
-                                           float& M1, float& M2, int& C1) {
-    const int j0 = c * kChunk;
-    float ca = INFINITY, cb = INFINITY;   // two partial minima: half the dependency chain
-#pragma unroll 4
-    for (int j = j0; j < j0 + kChunk; j += 4) {
-        const float4 p0 = *reinterpret_cast<const float4*>(candf + j);
-        const float4 p1 = *reinterpret_cast<const float4*>(candf + j + 2);
-        ca = fminf(ca, fminf(screen_d32(p0.x, p0.y, qx, qy), screen_d32(p0.z, p0.w, qx, qy)));
-        cb = fminf(cb, fminf(screen_d32(p1.x, p1.y, qx, qy), screen_d32(p1.z, p1.w, qx, qy)));
-    }
-    take_chunk(fminf(ca, cb), c, M1, M2, C1);
-}
-
 // Conservative squared distance between two axis-aligned boxes (or a point,
 // as a degenerate box), rounded DOWN by 1e-6 relative: a lower bound of every
 // fp32 screened distance between their points (>> the ~16 u of rounding).
@@ -304,7 +300,7 @@ __device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, 
     const bool lt = d < M1;
     M2 = __builtin_amdgcn_fmed3f(M1, M2, d);
     J1 = lt ? j : J1;
-    M1 = fminf(M1, d);
+    M1 = __builtin_amdgcn_fmed3f(M1, d, -INFINITY);   // min of non-NaN values, no canonicalisation
 }
 
 // Clearance state carried across ICP iterations, one 32-bit word per query:
@@ -354,8 +350,9 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
             const float4 pp = *reinterpret_cast<const float4*>(candf + ws[k] * kSub + t);
-            take_cand(screen_d32(pp.x, pp.y, qx[k], qy[k]), t, M1[k], M2[k], J1[k]);
-            take_cand(screen_d32(pp.z, pp.w, qx[k], qy[k]), t + 1, M1[k], M2[k], J1[k]);
+            const f32x2v d = screen_pair(pp, qx[k], qy[k]);
+            take_cand(d.x, t, M1[k], M2[k], J1[k]);
+            take_cand(d.y, t + 1, M1[k], M2[k], J1[k]);
         }
     }
 #pragma unroll
@@ -472,8 +469,9 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 #pragma unroll
                         for (int t = 0; t < kSub; t += 2) {
                             const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
-                            take_cand(screen_d32(pp.x, pp.y, qx[k], qy[k]), c8 + t, M1[k], M2[k], J1[k]);
-                            take_cand(screen_d32(pp.z, pp.w, qx[k], qy[k]), c8 + t + 1, M1[k], M2[k], J1[k]);
+                            const f32x2v d = screen_pair(pp, qx[k], qy[k]);
+                            take_cand(d.x, c8 + t, M1[k], M2[k], J1[k]);
+                            take_cand(d.y, c8 + t + 1, M1[k], M2[k], J1[k]);
                         }
                     }
                 }
@@ -541,13 +539,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             const double2 p = p2[j];
             cand[j] = p;
             if constexpr (SCREEN) {
-                candf[j] = make_float2(static_cast<float>(p.x), static_cast<float>(p.y));
+                cf_put(candf, j, static_cast<float>(p.x), static_cast<float>(p.y));
                 cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
             }
         }
         if constexpr (SCREEN) {
             for (int j = n2 + tid; j < (n2 + kChunk - 1) / kChunk * kChunk; j += BLOCK)
-                candf[j] = make_float2(kSentinel, kSentinel);
+                cf_put(candf, j, kSentinel, kSentinel);
         }
     }
     const int nsub = (n2 + kChunk - 1) / kChunk * (kChunk / kSub);   // sub-chunks incl. padding
@@ -556,7 +554,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         for (int c = tid; c < nsub; c += BLOCK) {
             float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
             for (int j = c * kSub; j < min(n2, (c + 1) * kSub); ++j) {
-                const float2 p = candf[j];
+                const float2 p = cf_at(candf, j);
                 x0 = fminf(x0, p.x);
                 x1 = fmaxf(x1, p.x);
                 y0 = fminf(y0, p.y);
@@ -733,7 +731,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         float b1 = INFINITY;
 #pragma unroll 2
                         for (int j = C1[k]; j < C1[k] + kChunk; ++j) {
-                            const float2 p = candf[j];
+                            const float2 p = cf_at(candf, j);
                             const float d = screen_d32(p.x, p.y, fx[k], fy[k]);
                             b2 = __builtin_amdgcn_fmed3f(b1, b2, d);
                             if (d < b1) j1 = j;

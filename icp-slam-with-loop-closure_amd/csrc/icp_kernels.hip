@@ -296,11 +296,16 @@ constexpr int kBatch = SLAM_BATCH;   // live sub-chunks tested per batch
 #define SLAM_WPE320 1
 #endif
 
+// Screened distances are non-negative (or +inf), so their IEEE bit patterns
+// order like unsigned integers: the updates run on the bits (integer min /
+// med3 need no NaN canonicalisation of the loop-carried M1, M2).
 __device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, int& J1) {
-    const bool lt = d < M1;
-    M2 = __builtin_amdgcn_fmed3f(M1, M2, d);
-    J1 = lt ? j : J1;
-    M1 = __builtin_amdgcn_fmed3f(M1, d, -INFINITY);   // min of non-NaN values, no canonicalisation
+    const uint32_t db = __float_as_uint(d), m1 = __float_as_uint(M1), m2 = __float_as_uint(M2);
+    J1 = db < m1 ? j : J1;
+    uint32_t md;   // second smallest of {M1 <= M2, d}
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(md) : "v"(m1), "v"(m2), "v"(db));
+    M2 = __uint_as_float(md);
+    M1 = __uint_as_float(min(m1, db));
 }
 
 // Clearance state carried across ICP iterations, one 32-bit word per query:

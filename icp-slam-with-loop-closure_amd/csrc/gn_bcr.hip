@@ -27,6 +27,9 @@
 namespace slamhip {
 
 constexpr int kBcrThreads = 256;
+#ifndef SLAM_ELIM_UNROLL
+#define SLAM_ELIM_UNROLL 2   // pivots per unrolled step of the register elimination (A/B)
+#endif
 constexpr int kBcrMaxWb = 96;
 
 __host__ __device__ inline int64_t bcr_blk(int Wb) { return static_cast<int64_t>(Wb) * Wb; }
@@ -74,6 +77,7 @@ __device__ __forceinline__ void bcr_reg_elim(double (&a)[T][T], double (&r)[T][N
                                              double (*rowb)[16 * NW], int tr, int tc, bool& bad, double* rdg) {
 #pragma unroll
     for (int kv = 0; kv < T; ++kv) {
+#pragma unroll SLAM_ELIM_UNROLL
         for (int kk = 0; kk < 16; ++kk) {
             const int k = 16 * kv + kk, kb = k & 1;
             if (tc == kk) {   // column k of D_i (all rows; rows < k are never read)

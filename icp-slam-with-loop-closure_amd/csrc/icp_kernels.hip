@@ -285,7 +285,7 @@ constexpr int kSub = 8;
 #endif
 constexpr int kWin = SLAM_WIN;
 #ifndef SLAM_BATCH
-#define SLAM_BATCH 4
+#define SLAM_BATCH 3
 #endif
 constexpr int kBatch = SLAM_BATCH;   // live sub-chunks tested per batch
 // waves/SIMD the default 1081-point instances are compiled for (A/B builds override)

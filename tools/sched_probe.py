@@ -1,6 +1,7 @@
 """How much of the C3 batch time is the long-tail of slow-converging pairs:
 the same pairs launched in natural order, in descending order of their
-(known) iteration counts, and ascending.  GPU only."""
+(known) iteration counts, and ascending — as one launch (scheduler off) and
+through the two-phase scheduler.  GPU only."""
 import os
 import sys
 
@@ -18,8 +19,12 @@ inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i i
 ss = k.ScanSet(seq.scans)
 src, dst = np.arange(1, pairs + 1), np.arange(0, pairs)
 r = k.icp_batch(ss, src, dst, inits, epsilon=0.05, max_iters=100)
-for name, perm in (("natural", np.arange(pairs)), ("desc", np.argsort(-r.iters, kind="stable")),
-                   ("asc", np.argsort(r.iters, kind="stable"))):
+from slamhip import _abi  # noqa: E402
+lib = _abi.lib()
+for name, perm, probe in (("natural", np.arange(pairs), 0), ("desc", np.argsort(-r.iters, kind="stable"), 0),
+                          ("asc", np.argsort(r.iters, kind="stable"), 0), ("natural+scheduler", np.arange(pairs), 5),
+                          ("desc+scheduler", np.argsort(-r.iters, kind="stable"), 5)):
+    lib.slam_icp_set_schedule(probe, 2048)
     b = k.IcpBatch(ss, src[perm], dst[perm], inits[perm], epsilon=0.05, max_iters=100)
     b.launch()
     ts = []

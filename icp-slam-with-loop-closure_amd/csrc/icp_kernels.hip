@@ -954,11 +954,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
                     a.out_iters[b] = -(it + 1);
-#if SLAM_SCHED_KEY == 1
-                    a.sched_key[b] = static_cast<float>(err);
-#else
                     a.sched_key[b] = static_cast<float>(derr);
-#endif
                 }
                 return;
             }
@@ -1118,15 +1114,6 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
-#ifndef SLAM_SCHED_NMID
-#define SLAM_SCHED_NMID 0   // capped middle phases between the probe and the final phase (A/B)
-#endif
-#ifndef SLAM_SCHED_MID
-#define SLAM_SCHED_MID 12
-#endif
-#ifndef SLAM_SCHED_KEY
-#define SLAM_SCHED_KEY 0   // 0: last error change, 1: error level (A/B)
-#endif
 static int g_sched_probe = 5;          // phase-1 iterations (0: single launch; 4-6 best on C3)
 static int g_sched_min_pairs = 2048;   // batches below this fit the GPU in ~2 waves
 
@@ -1180,21 +1167,17 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     a.phase_cap = probe;
     a.sched_key = key;
     int rc = launch(false, a, B, max_n1, max_n2, stream);
-    const int g = (B + 255) / 256;
-#if SLAM_SCHED_KEY == 1
-    const float thr = 1.0f;
-#else
-    const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
-#endif
-    // optional capped middle phases (A/B: SLAM_SCHED_MID iterations each), then the rest
-    for (int ph = 0; rc == 0 && ph <= SLAM_SCHED_NMID; ++ph) {
+    if (rc == 0) {
+        const int g = (B + 255) / 256;
+        const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
         (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
         hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
         hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);
         hipLaunchKernelGGL(sched_scatter_kernel, dim3(g), dim3(256), 0, s, bucket, B, hist, order);
         rc = check_launch("icp scheduler kernels");
-        if (rc != 0) break;
-        a.phase_cap = ph < SLAM_SCHED_NMID ? SLAM_SCHED_MID : 0;
+    }
+    if (rc == 0) {   // phase 2: the unfinished pairs, slowest-converging first
+        a.phase_cap = 0;
         a.resume = 1;
         a.order = order;
         rc = launch(false, a, B, max_n1, max_n2, stream);

@@ -305,14 +305,23 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
 // Backward substitution C^T x = v by one wave, C lower in LDS (stride ldc);
 // v in lanes (rows lane, lane + 64); returns x in the same layout.
 __device__ inline void bcr_backsub_wave(const double* Cm, int ldc, const double* rdg, int Wb, double& v0, double& v1) {
+    // lane j holds 1 / C[j][j] (and j + 64): x_k = v_k / C_kk is formed in lane
+    // k and broadcast by one v_readlane — no LDS read on the dependent chain;
+    // rows >= 64 first, so every branch below is wave-uniform
     const int lane = threadIdx.x & 63;
-    for (int k = Wb - 1; k >= 0; --k) {
-        const double vk = k < 64 ? readlane_d(v0, k) : readlane_d(v1, k - 64);
-        const double xk = vk * rdg[k];
-        if (lane == k) v0 = xk;
+    const double r0 = lane < Wb ? rdg[lane] : 0.0, r1 = lane + 64 < Wb ? rdg[lane + 64] : 0.0;
+    for (int k = Wb - 1; k >= 64; --k) {
+        const double xk = readlane_d(v1 * r1, k - 64);
+        const double c0 = Cm[k * ldc + lane], c1 = Cm[k * ldc + lane + 64];
         if (lane + 64 == k) v1 = xk;
-        if (lane < k) v0 = fma(-Cm[k * ldc + lane], xk, v0);
-        if (lane + 64 < k) v1 = fma(-Cm[k * ldc + lane + 64], xk, v1);
+        if (lane + 64 < k) v1 = fma(-c1, xk, v1);
+        v0 = fma(-c0, xk, v0);
+    }
+    for (int k = min(Wb, 64) - 1; k >= 0; --k) {
+        const double xk = readlane_d(v0 * r0, k);
+        const double c0 = Cm[k * ldc + lane];
+        if (lane == k) v0 = xk;
+        if (lane < k) v0 = fma(-c0, xk, v0);
     }
 }
 

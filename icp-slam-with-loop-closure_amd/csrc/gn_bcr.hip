@@ -220,7 +220,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     const bool hE = part == 1 && i2 < nb && j + 2 * s < nb;
     const bool h1 = part == 0 && i1 >= 0, h2 = (part == 0 && i2 < nb) || hE;
     if (!h1 && !h2) return;
-    const float inv = 1.0f / static_cast<float>(Wb);
     const int64_t B2 = bcr_blk(Wb);
     double acc[T][T], accE[T][T];
 #pragma unroll
@@ -237,11 +236,21 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     {
         const double* S1 = part == 0 ? (h1 ? Ys + i1 * B2 : nullptr) : Xs + i2 * B2;
         const double* S2 = part == 0 ? (h2 ? Xs + i2 * B2 : nullptr) : Ys + i2 * B2;
-        for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-            int r, c;
-            bcr_rc(e, Wb, inv, r, c);
-            L1[r * ld + c] = S1 ? S1[e] : 0.0;
-            L2[r * ld + c] = S2 ? S2[e] : 0.0;
+        // compile-time trip count ((16T)^2 / 256 = T^2 per thread): every global
+        // load is issued before the first LDS store (one memory latency, not T^2)
+        constexpr int WB = 16 * T;
+        double g1[T * T], g2[T * T];
+#pragma unroll
+        for (int q = 0; q < T * T; ++q) {
+            const int e = tid + kBcrThreads * q;
+            g1[q] = S1 ? S1[e] : 0.0;
+            g2[q] = S2 ? S2[e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < T * T; ++q) {
+            const int e = tid + kBcrThreads * q, r = e / WB, c = e % WB;
+            L1[r * ld + c] = g1[q];
+            L2[r * ld + c] = g2[q];
         }
         if (part == 0)
             for (int r = tid; r < Wb; r += kBcrThreads) {
@@ -398,11 +407,16 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
     const int p = i - s, n = i + s;
     const int64_t B2 = bcr_blk(Wb);
     const double* Ci = Cs + i * B2;
-    const float inv = 1.0f / static_cast<float>(Wb);
-    for (int e = tid; e < Wb * Wb; e += kBcrThreads) {
-        int r, c;
-        bcr_rc(e, Wb, inv, r, c);
-        Cm[r * ldc + c] = Ci[e];
+    {
+        constexpr int WB = 16 * T;   // compile-time trip count: all loads in flight at once
+        double g[T * T];
+#pragma unroll
+        for (int q = 0; q < T * T; ++q) g[q] = Ci[tid + kBcrThreads * q];
+#pragma unroll
+        for (int q = 0; q < T * T; ++q) {
+            const int e = tid + kBcrThreads * q;
+            Cm[(e / WB) * ldc + e % WB] = g[q];
+        }
     }
     for (int k = tid; k < Wb; k += kBcrThreads) {
         rdg[k] = 1.0 / Ci[static_cast<int64_t>(k) * Wb + k];

@@ -274,6 +274,9 @@ constexpr int kSub = 8;
 #ifndef SLAM_WIN
 #define SLAM_WIN 4
 #endif
+#ifndef SLAM_STAGE_UNROLL
+#define SLAM_STAGE_UNROLL 4
+#endif
 #ifndef SLAM_SHIFT
 #define SLAM_SHIFT 1
 #endif
@@ -540,7 +543,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 
     double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound)
     if (resident) {
-        for (int j = tid; j < n2; j += BLOCK) {
+#pragma unroll SLAM_STAGE_UNROLL
+        for (int j = tid; j < n2; j += BLOCK) {   // unrolled: several loads in flight per thread
             const double2 p = p2[j];
             cand[j] = p;
             if constexpr (SCREEN) {
@@ -581,6 +585,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     if constexpr (SCREEN) {
         double cm[2] = {cmax, 0.0};
         if constexpr (PRUNE) {
+#pragma unroll SLAM_STAGE_UNROLL
             for (int i = tid; i < n1; i += BLOCK) {
                 const double2 p = p1[i];
                 cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));

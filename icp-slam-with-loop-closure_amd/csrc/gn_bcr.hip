@@ -89,7 +89,17 @@ __device__ __forceinline__ void bcr_reg_elim(double (&a)[T][T], double (&r)[T][N
                 for (int w = 0; w < NW; ++w) rowb[kb][tc + 16 * w] = r[kv][w];
             }
             __syncthreads();
+            // every broadcast value is read at once, unconditionally (one LDS
+            // latency), then the pivot's reciprocal square root
             const double piv = colb[kb][k];
+            double cr[T], cc[T], cz[NW];
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                cr[u] = colb[kb][tr + 16 * u];
+                cc[u] = colb[kb][tc + 16 * u];
+            }
+#pragma unroll
+            for (int w = 0; w < NW; ++w) cz[w] = rowb[kb][tc + 16 * w];
             bad |= !(piv > 0.0);
             const double rd = rsqrt(piv);   // reciprocal pivot: no fp64 division on the chain
             if (rdg && tr == kk && tc == kk) rdg[k] = rd;
@@ -97,13 +107,11 @@ __device__ __forceinline__ void bcr_reg_elim(double (&a)[T][T], double (&r)[T][N
             double lr[T], lc[T], z[NW];
 #pragma unroll
             for (int u = 0; u < T; ++u) {
-                const int R = tr + 16 * u;
-                lr[u] = colb[kb][R] * rd;                    // L[R][k] for R > k
-                const int C = tc + 16 * u;
-                lc[u] = C > k ? colb[kb][C] * rd : 0.0;      // L[C][k], columns still to update
+                lr[u] = cr[u] * rd;                                  // L[R][k] for R > k
+                lc[u] = tc + 16 * u > k ? cc[u] * rd : 0.0;          // L[C][k], columns still to update
             }
 #pragma unroll
-            for (int w = 0; w < NW; ++w) z[w] = rowb[kb][tc + 16 * w] * rd;   // z_k
+            for (int w = 0; w < NW; ++w) z[w] = cz[w] * rd;   // z_k
 #pragma unroll
             for (int u = 0; u < T; ++u) {
                 const int R = tr + 16 * u;

@@ -274,6 +274,9 @@ constexpr int kSub = 8;
 #ifndef SLAM_WIN
 #define SLAM_WIN 4
 #endif
+#ifndef SLAM_PREFETCH
+#define SLAM_PREFETCH 1   // winners and matches of all groups loaded at once (A/B: 0)
+#endif
 #ifndef SLAM_STAGE_UNROLL
 #define SLAM_STAGE_UNROLL 4
 #endif
@@ -721,6 +724,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 }
                 stamp(0);
                 // ---- certify: the screened winner is the exact fp64 argmin? ---
+#if SLAM_PREFETCH
+                // the winners' fp64 coordinates for every group at once: one LDS
+                // latency instead of one per (divergent) certification branch
+                double2 cw[QPT];
+                if constexpr (PRUNE) {
+#pragma unroll
+                    for (int k = 0; k < QPT; ++k) cw[k] = cand[min(C1[k], n2 - 1)];
+                }
+#endif
 #pragma unroll
                 for (int k = 0; k < QPT; ++k) {
                     const int i = k * BLOCK + tid;
@@ -754,7 +766,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     if (!screen) {
                         ok = i >= n1;   // |coordinates| >= 1e18: every query takes the exact path
                     } else if (i < n1 && n2 > 1) {
+#if SLAM_PREFETCH
+                        const double2 c = PRUNE ? cw[k] : cand[j1];
+#else
                         const double2 c = cand[j1];
+#endif
                         const double d1 = exact_d2(c.x, c.y, qx[k], qy[k]);
                         const double s2 = static_cast<double>(fminf(M2[k], b2));   // every other j: d32 >= s2
                         const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
@@ -840,11 +856,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 
         // ---- src/icp.py:64,68  centroids + error ------------------------------
         double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#if SLAM_PREFETCH
+        double2 mk[QPT];   // matched points of every group at once (one memory latency)
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) mk[k] = resident ? cand[bi[k]] : p2[bi[k]];
+#endif
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
             const int i = k * BLOCK + tid;
             if (i < n1) {
+#if SLAM_PREFETCH
+                const double2 m = mk[k];
+#else
                 const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
+#endif
                 v[0] += qx[k];
                 v[1] += qy[k];
                 v[2] += m.x;

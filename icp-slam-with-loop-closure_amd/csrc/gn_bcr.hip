@@ -220,7 +220,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     double* L2 = lds + static_cast<int64_t>(Wb) * ld;   // [Wb][Wb + 1]
     double* zv = L2 + static_cast<int64_t>(Wb) * ld;    // [2][Wb]
     const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
-    constexpr int nt = T;
     const int j = 2 * s * blockIdx.x;
     const int i1 = j - s, i2 = j + s;
     // part 0 (blockIdx.y): D_j and b_j updates; part 1: the new coupling E'_j
@@ -306,16 +305,24 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     }
     double* Dj = D + j * B2;
     double* Ej = E + j * B2;
+    constexpr int WB = 16 * T;   // compile-time row stride: provably distinct addresses
+    if (hE) {
 #pragma unroll
-    for (int u = 0; u < T; ++u)
+        for (int u = 0; u < T; ++u)
 #pragma unroll
-        for (int v = 0; v < T; ++v) {
-            if (u < nt && v < nt) {
-                const int r = tr + 16 * u, c = tc + 16 * v;
-                if (hE) Ej[r * Wb + c] = -accE[u][v];
-                else Dj[r * Wb + c] -= acc[u][v];
-            }
-        }
+            for (int v = 0; v < T; ++v) Ej[(tr + 16 * u) * WB + tc + 16 * v] = -accE[u][v];
+    } else {
+        // every D_j load issued before the first store (no load/store chain)
+        double dv[T][T];
+#pragma unroll
+        for (int u = 0; u < T; ++u)
+#pragma unroll
+            for (int v = 0; v < T; ++v) dv[u][v] = Dj[(tr + 16 * u) * WB + tc + 16 * v];
+#pragma unroll
+        for (int u = 0; u < T; ++u)
+#pragma unroll
+            for (int v = 0; v < T; ++v) Dj[(tr + 16 * u) * WB + tc + 16 * v] = dv[u][v] - acc[u][v];
+    }
     if (part == 0 && tid < Wb) bz[static_cast<int64_t>(j) * Wb + tid] -= bacc;
 }
 

@@ -57,6 +57,9 @@ __device__ __forceinline__ M3 m3_transpose(const M3& x) {
 
 // Inverse by LU with partial pivoting (dgesv on the identity), enough for the
 // well-conditioned R sigma R^T blocks here.
+#ifndef SLAM_SGD_FAST
+#define SLAM_SGD_FAST 1   // relaxation chain: closed-form inverse, reciprocal total weights (A/B: 0)
+#endif
 __device__ __forceinline__ M3 m3_inv(const M3& m) {
     double A[3][3], X[3][3];
 #pragma unroll
@@ -90,6 +93,28 @@ __device__ __forceinline__ M3 m3_inv(const M3& m) {
             for (int k = i + 1; k < 3; ++k) s -= A[i][k] * r.a[k][j];
             r.a[i][j] = s / A[i][i];
         }
+    return r;
+}
+
+// Closed-form 3x3 inverse (adjugate times one reciprocal of the determinant):
+// the relaxation's dependent chain keeps one fp64 division instead of the
+// nine of the pivoted LU (agrees with it to rounding; tests at 1e-9).
+__device__ __forceinline__ M3 m3_inv_adj(const M3& m) {
+    const double(&a)[3][3] = m.a;
+    const double c00 = fma(a[1][1], a[2][2], -a[1][2] * a[2][1]);
+    const double c01 = fma(a[1][2], a[2][0], -a[1][0] * a[2][2]);
+    const double c02 = fma(a[1][0], a[2][1], -a[1][1] * a[2][0]);
+    const double id = 1.0 / fma(a[0][0], c00, fma(a[0][1], c01, a[0][2] * c02));
+    M3 r;
+    r.a[0][0] = c00 * id;
+    r.a[1][0] = c01 * id;
+    r.a[2][0] = c02 * id;
+    r.a[0][1] = fma(a[0][2], a[2][1], -a[0][1] * a[2][2]) * id;
+    r.a[1][1] = fma(a[0][0], a[2][2], -a[0][2] * a[2][0]) * id;
+    r.a[2][1] = fma(a[0][1], a[2][0], -a[0][0] * a[2][1]) * id;
+    r.a[0][2] = fma(a[0][1], a[1][2], -a[0][2] * a[1][1]) * id;
+    r.a[1][2] = fma(a[0][2], a[1][0], -a[0][0] * a[1][2]) * id;
+    r.a[2][2] = fma(a[0][0], a[1][1], -a[0][1] * a[1][0]) * id;
     return r;
 }
 
@@ -337,7 +362,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
     // Edge k's pose-independent operands are loaded during edge k-1.
     struct Pre {
         int a, b, ni;
-        double z[9], ca[3], cb[3], ci[3];
+        double z[9], ca[3], cb[3], ci[3], irtw[3];
     };
     auto fetch = [&](int k, Pre& q) {
         q.a = A[k];
@@ -351,6 +376,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             q.ca[j] = C[3 * (q.a + 1) + j];
             q.cb[j] = C[3 * (q.b + 1) + j];
             q.ci[j] = C[3 * (i0 + 1) + j];
+            q.irtw[j] = 1.0 / (q.cb[j] - q.ca[j]);   // pose-independent: off the dependent chain
         }
     };
     Pre cur, nxt;
@@ -379,7 +405,11 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
         r[0] = Pb.a[0][2] - pb[0];
         r[1] = Pb.a[1][2] - pb[1];
         r[2] = py_mod(atan2(Pb.a[1][0], Pb.a[0][0]) - pb[2], TWO_PI);
+#if SLAM_SGD_FAST
+        const M3 Wi = m3_inv_adj(m3_mul(m3_mul(m3_transpose(R), S), R));
+#else
         const M3 Wi = m3_inv(m3_mul(m3_mul(m3_transpose(R), S), R));
+#endif
         double beta[3], rtw[3];
         const int L = b - a;
 #pragma unroll
@@ -399,7 +429,11 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             while (i >= 0) {
                 if (i <= b) {
 #pragma unroll
+#if SLAM_SGD_FAST
+                    for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) * cur.irtw[j]);
+#else
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) / rtw[j]);
+#endif
                 } else {
 #pragma unroll
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
@@ -419,7 +453,11 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             if (q < bb) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
+#if SLAM_SGD_FAST
+                    const double g = beta[j] * cur.irtw[j];
+#else
                     const double g = beta[j] / rtw[j];
+#endif
                     cA[3 * q + j] += g;
                     off[3 * q + j] -= g * cur.ca[j];
                 }

@@ -21,6 +21,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -222,8 +223,11 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
     const int j = 2 * s * blockIdx.x;
     const int i1 = j - s, i2 = j + s;
-    // part 0 (blockIdx.y): D_j and b_j updates; part 1: the new coupling E'_j
-    const int part = blockIdx.y;
+    // blockIdx.y: 0 / 2 -> part 0 (D_j, b_j updates), rows tr + 16u with u < UH / u >= UH
+    // (two workgroups share the critical part-0 products); 1 -> part 1 (new coupling E'_j)
+    const int part = blockIdx.y == 1 ? 1 : 0;
+    const bool upper = blockIdx.y == 2;
+    constexpr int UH = (T + 1) / 2;
     const bool hE = part == 1 && i2 < nb && j + 2 * s < nb;
     const bool h1 = part == 0 && i1 >= 0, h2 = (part == 0 && i2 < nb) || hE;
     if (!h1 && !h2) return;
@@ -266,21 +270,28 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
             }
         __syncthreads();
         if (part == 0) {
-            for (int k = 0; k < Wb; ++k) {
-                double a1[T], b1[T], a2[T], b2[T];
+            auto rows = [&](auto lo_c, auto hi_c) {   // compile-time row-tile range [lo, hi)
+                constexpr int lo = decltype(lo_c)::value, hi = decltype(hi_c)::value;
+                for (int k = 0; k < Wb; ++k) {
+                    double a1[T], b1[T], a2[T], b2[T];
 #pragma unroll
-                for (int u = 0; u < T; ++u) {
-                    a1[u] = L1[k * ld + tr + 16 * u];
-                    b1[u] = L1[k * ld + tc + 16 * u];
-                    a2[u] = L2[k * ld + tr + 16 * u];
-                    b2[u] = L2[k * ld + tc + 16 * u];
+                    for (int u = 0; u < T; ++u) {
+                        if (u >= lo && u < hi) {
+                            a1[u] = L1[k * ld + tr + 16 * u];
+                            a2[u] = L2[k * ld + tr + 16 * u];
+                        }
+                        b1[u] = L1[k * ld + tc + 16 * u];
+                        b2[u] = L2[k * ld + tc + 16 * u];
+                    }
+#pragma unroll
+                    for (int u = lo; u < hi; ++u)
+#pragma unroll
+                        for (int v = 0; v < T; ++v) acc[u][v] = fma(a2[u], b2[v], fma(a1[u], b1[v], acc[u][v]));
                 }
-#pragma unroll
-                for (int u = 0; u < T; ++u)
-#pragma unroll
-                    for (int v = 0; v < T; ++v) acc[u][v] = fma(a2[u], b2[v], fma(a1[u], b1[v], acc[u][v]));
-            }
-            if (tid < Wb) {
+            };
+            if (upper) rows(std::integral_constant<int, UH>{}, std::integral_constant<int, T>{});
+            else rows(std::integral_constant<int, 0>{}, std::integral_constant<int, UH>{});
+            if (!upper && tid < Wb) {
                 double b2acc = 0.0;
                 for (int k = 0; k < Wb; ++k) {
                     bacc = fma(L1[k * ld + tid], zv[k], bacc);
@@ -312,18 +323,22 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
 #pragma unroll
             for (int v = 0; v < T; ++v) Ej[(tr + 16 * u) * WB + tc + 16 * v] = -accE[u][v];
     } else {
-        // every D_j load issued before the first store (no load/store chain)
+        // every D_j load issued before the first store (no load/store chain); this
+        // workgroup's row tiles only
+        const int ulo = upper ? UH : 0, uhi = upper ? T : UH;
         double dv[T][T];
 #pragma unroll
         for (int u = 0; u < T; ++u)
 #pragma unroll
-            for (int v = 0; v < T; ++v) dv[u][v] = Dj[(tr + 16 * u) * WB + tc + 16 * v];
+            for (int v = 0; v < T; ++v)
+                if (u >= ulo && u < uhi) dv[u][v] = Dj[(tr + 16 * u) * WB + tc + 16 * v];
 #pragma unroll
         for (int u = 0; u < T; ++u)
 #pragma unroll
-            for (int v = 0; v < T; ++v) Dj[(tr + 16 * u) * WB + tc + 16 * v] = dv[u][v] - acc[u][v];
+            for (int v = 0; v < T; ++v)
+                if (u >= ulo && u < uhi) Dj[(tr + 16 * u) * WB + tc + 16 * v] = dv[u][v] - acc[u][v];
     }
-    if (part == 0 && tid < Wb) bz[static_cast<int64_t>(j) * Wb + tid] -= bacc;
+    if (part == 0 && !upper && tid < Wb) bz[static_cast<int64_t>(j) * Wb + tid] -= bacc;
 }
 
 // Backward substitution C^T x = v by one wave, C lower in LDS (stride ldc);
@@ -553,7 +568,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
         hipLaunchKernelGGL(odd, dim3(n_odd, 2), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
                            stamps);
-        hipLaunchKernelGGL(even, dim3(n_even, 2), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
+        hipLaunchKernelGGL(even, dim3(n_even, 3), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }
     hipLaunchKernelGGL(top, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
     for (s /= 2; s >= 1; s /= 2) {

@@ -150,20 +150,28 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
                                                                   int32_t Wb, int32_t nb, int32_t s,
                                                                   int32_t* __restrict__ status,
                                                                   unsigned long long* __restrict__ stamps) {
-    constexpr int NW = T + 1;   // column tiles of R (part 1: Wb + 1 columns)
+    // four workgroups per odd block (blockIdx.y = q): each eliminates D_i and carries
+    // NW of the 2T + 1 right-hand-side column tiles — q 0, 1: tiles [0, NW), [NW, T) of
+    // E_p (-> X_i); q 2, 3: tiles [0, NW), [NW, T + 1) of [E_i^T | b_i] (-> Y_i, z_i).
+    // Fewer tiles per workgroup = less work per pivot on the dependent chain.
+    constexpr int NW = (T + 2) / 2;
     __shared__ double colb[2][16 * T];
     __shared__ double rowb[2][16 * NW];
-    const bool stamping = stamps && blockIdx.x == 0 && blockIdx.y == 1 && threadIdx.x == 0;
+    const int q = blockIdx.y;
+    const bool ys = q >= 2;                    // Y side (E_i^T | b_i)
+    const int w0 = (q & 1) ? NW : 0;           // first global column tile
+    const int wend = (q & 1) ? (ys ? T + 1 : T) : NW;
+    const bool owner = q == 2;                 // writes C_i and the status
+    const bool stamping = stamps && blockIdx.x == 0 && owner && threadIdx.x == 0;
     unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
-    auto lap = [&](int q) {
+    auto lap = [&](int qq) {
         if (stamping) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-            stamps[q] += t1 - t0;
+            stamps[qq] += t1 - t0;
             t0 = t1;
         }
     };
     const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
-    const int part = blockIdx.y;
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
     const int64_t B2 = bcr_blk(Wb);
@@ -173,33 +181,42 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
     double a[T][T], r[T][NW];
 #pragma unroll
     for (int u = 0; u < T; ++u) {
+        const int R = tr + 16 * u;
 #pragma unroll
-        for (int v = 0; v < T; ++v) a[u][v] = Di[(tr + 16 * u) * Wb + tc + 16 * v];
+        for (int v = 0; v < T; ++v) a[u][v] = Di[R * Wb + tc + 16 * v];
 #pragma unroll
-        for (int w = 0; w < T; ++w) {
-            const int R = tr + 16 * u, C = tc + 16 * w;
-            r[u][w] = part == 0 ? Ep[R * Wb + C] : (n < nb ? Ei[C * Wb + R] : 0.0);
+        for (int wl = 0; wl < NW; ++wl) {
+            const int w = w0 + wl, C = tc + 16 * w;
+            double x = 0.0;
+            if (w < wend) {
+                if (!ys) x = Ep[R * Wb + C];
+                else if (w < T) x = n < nb ? Ei[C * Wb + R] : 0.0;
+                else x = tc == 0 ? bz[static_cast<int64_t>(i) * Wb + R] : 0.0;
+            }
+            r[u][wl] = x;
         }
-        r[u][T] = (part == 1 && tc == 0) ? bz[static_cast<int64_t>(i) * Wb + tr + 16 * u] : 0.0;
     }
     lap(0);
     bool bad = false;
     bcr_reg_elim<T, NW>(a, r, colb, rowb, tr, tc, bad, nullptr);
     lap(1);
-    if (bad && part == 1 && tid == 0) *status = 1;
-    double* Out = (part == 0 ? Xs : Ys) + i * B2;
+    if (bad && owner && tid == 0) *status = 1;
+    double* Out = (ys ? Ys : Xs) + i * B2;
 #pragma unroll
     for (int u = 0; u < T; ++u) {
         const int R = tr + 16 * u;
 #pragma unroll
-        for (int w = 0; w < T; ++w) Out[R * Wb + tc + 16 * w] = r[u][w];
-        if (part == 1) {
+        for (int wl = 0; wl < NW; ++wl) {
+            const int w = w0 + wl;
+            if (w < wend && w < T) Out[R * Wb + tc + 16 * w] = r[u][wl];
+            if (w < wend && w == T && tc == 0) bz[static_cast<int64_t>(i) * Wb + R] = r[u][wl];
+        }
+        if (owner) {
 #pragma unroll
             for (int v = 0; v < T; ++v) {
                 const int C = tc + 16 * v;
                 Cs[i * B2 + R * Wb + C] = C <= R ? a[u][v] : 0.0;
             }
-            if (tc == 0) bz[static_cast<int64_t>(i) * Wb + R] = r[u][T];
         }
     }
     lap(3);
@@ -566,7 +583,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     for (; s < nb; s *= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
-        hipLaunchKernelGGL(odd, dim3(n_odd, 2), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
+        hipLaunchKernelGGL(odd, dim3(n_odd, 4), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
                            stamps);
         hipLaunchKernelGGL(even, dim3(n_even, 3), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }

@@ -240,11 +240,16 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
     const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
     const int j = 2 * s * blockIdx.x;
     const int i1 = j - s, i2 = j + s;
-    // blockIdx.y: 0 / 2 -> part 0 (D_j, b_j updates), rows tr + 16u with u < UH / u >= UH
-    // (two workgroups share the critical part-0 products); 1 -> part 1 (new coupling E'_j)
-    const int part = blockIdx.y == 1 ? 1 : 0;
-    const bool upper = blockIdx.y == 2;
-    constexpr int UH = (T + 1) / 2;
+    // blockIdx.y splits the work by row tiles u of the outputs: part 0 (D_j, b_j updates:
+    // two products) over y = 0, 2, 3 -> u in [0, A), [A, B), [B, T); part 1 (new coupling
+    // E'_j: one product) over y = 1, 4 -> u in [0, C), [C, T)
+    constexpr int A = (T + 2) / 3, B = (2 * T + 2) / 3, C = (T + 1) / 2;
+    const int y = blockIdx.y;
+    const int part = (y == 1 || y == 4) ? 1 : 0;
+    const bool upper = y != 0 && y != 1;   // not the workgroup that owns the rhs update
+    const int ulo = y == 0 ? 0 : y == 1 ? 0 : y == 2 ? A : y == 3 ? B : C;
+    const int uhi = y == 0 ? A : y == 1 ? C : y == 2 ? B : T;
+    if (ulo >= uhi) return;   // empty row range (small T)
     const bool hE = part == 1 && i2 < nb && j + 2 * s < nb;
     const bool h1 = part == 0 && i1 >= 0, h2 = (part == 0 && i2 < nb) || hE;
     if (!h1 && !h2) return;
@@ -306,8 +311,9 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
                         for (int v = 0; v < T; ++v) acc[u][v] = fma(a2[u], b2[v], fma(a1[u], b1[v], acc[u][v]));
                 }
             };
-            if (upper) rows(std::integral_constant<int, UH>{}, std::integral_constant<int, T>{});
-            else rows(std::integral_constant<int, 0>{}, std::integral_constant<int, UH>{});
+            if (y == 0) rows(std::integral_constant<int, 0>{}, std::integral_constant<int, A>{});
+            else if (y == 2) rows(std::integral_constant<int, A>{}, std::integral_constant<int, B>{});
+            else rows(std::integral_constant<int, B>{}, std::integral_constant<int, T>{});
             if (!upper && tid < Wb) {
                 double b2acc = 0.0;
                 for (int k = 0; k < Wb; ++k) {
@@ -317,18 +323,23 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
                 bacc += b2acc;
             }
         } else {
-            for (int k = 0; k < Wb; ++k) {
-                double y[T], b[T];
+            auto rowsE = [&](auto lo_c, auto hi_c) {
+                constexpr int lo = decltype(lo_c)::value, hi = decltype(hi_c)::value;
+                for (int k = 0; k < Wb; ++k) {
+                    double yv[T], b[T];
 #pragma unroll
-                for (int u = 0; u < T; ++u) {
-                    y[u] = L2[k * ld + tr + 16 * u];
-                    b[u] = L1[k * ld + tc + 16 * u];
+                    for (int u = 0; u < T; ++u) {
+                        if (u >= lo && u < hi) yv[u] = L2[k * ld + tr + 16 * u];
+                        b[u] = L1[k * ld + tc + 16 * u];
+                    }
+#pragma unroll
+                    for (int u = lo; u < hi; ++u)
+#pragma unroll
+                        for (int v = 0; v < T; ++v) accE[u][v] = fma(yv[u], b[v], accE[u][v]);
                 }
-#pragma unroll
-                for (int u = 0; u < T; ++u)
-#pragma unroll
-                    for (int v = 0; v < T; ++v) accE[u][v] = fma(y[u], b[v], accE[u][v]);
-            }
+            };
+            if (y == 1) rowsE(std::integral_constant<int, 0>{}, std::integral_constant<int, C>{});
+            else rowsE(std::integral_constant<int, C>{}, std::integral_constant<int, T>{});
         }
     }
     double* Dj = D + j * B2;
@@ -338,11 +349,11 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_even_kernel(double* __restric
 #pragma unroll
         for (int u = 0; u < T; ++u)
 #pragma unroll
-            for (int v = 0; v < T; ++v) Ej[(tr + 16 * u) * WB + tc + 16 * v] = -accE[u][v];
+            for (int v = 0; v < T; ++v)
+                if (u >= ulo && u < uhi) Ej[(tr + 16 * u) * WB + tc + 16 * v] = -accE[u][v];
     } else {
         // every D_j load issued before the first store (no load/store chain); this
         // workgroup's row tiles only
-        const int ulo = upper ? UH : 0, uhi = upper ? T : UH;
         double dv[T][T];
 #pragma unroll
         for (int u = 0; u < T; ++u)
@@ -585,7 +596,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
         hipLaunchKernelGGL(odd, dim3(n_odd, 4), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
                            stamps);
-        hipLaunchKernelGGL(even, dim3(n_even, 3), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
+        hipLaunchKernelGGL(even, dim3(n_even, 5), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }
     hipLaunchKernelGGL(top, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
     for (s /= 2; s >= 1; s /= 2) {

@@ -5,14 +5,15 @@
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Workload (BASELINE.json configs[2], "Batched ICP: 10k synthetic scan-pairs x
-1081 pts"): every rank holds its own synthetic scan stream of P+1 scans
-(P = 10,000 by default; SURVEY.md §8(d) generator, seed 2025 + rank) already
-resident in HBM and runs ``icp()`` on the P consecutive pairs (i, i-1) with
-scripts/main.py's parameters (init = pose_to_mat(odom_i - odom_{i-1}),
-epsilon 0.05, max_iters 100).  One step = one ``slam_icp_batch_f64`` launch
-over the rank's P pairs and, for N > 1, the RCCL all-gather of the resulting
-SE(2) edges (the exchange step of the north star).  Per-GPU work is fixed as N
-grows ("scaling": "weak"); ``--strong`` shards one P-pair stream instead.
+1081 pts, 1->8 GPU sharding"): ONE synthetic scan stream of P+1 scans (P =
+10,000 by default; SURVEY.md §8(d) generator, seed 2025) whose P consecutive
+pairs (i, i-1) are sharded contiguously over the N ranks; each rank holds its
+shard resident in HBM and runs ``icp()`` on it with scripts/main.py's
+parameters (init = pose_to_mat(odom_i - odom_{i-1}), epsilon 0.05, max_iters
+100).  One step = one ``slam_icp_batch_f64`` launch over the rank's shard and,
+for N > 1, the RCCL all-gather of the resulting SE(2) edges (the exchange step
+of the north star).  Total work is fixed as N grows ("scaling": "strong");
+``--weak`` gives every rank its own P-pair stream (seed 2025 + rank) instead.
 
 Printed: ONE JSON line (rank 0) with the driver's contract fields plus
 ``roofline`` (dominant kernel: the FP32 VALU roofline over the candidate
@@ -49,13 +50,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--pairs", type=int, default=10000, help="scan pairs per rank (weak) or total (--strong)")
+    p.add_argument("--pairs", type=int, default=10000, help="scan pairs in total (default) or per rank (--weak)")
     p.add_argument("--beams", type=int, default=1081)
-    p.add_argument("--strong", action="store_true")
+    p.add_argument("--weak", action="store_true",
+                   help="every rank runs its own P-pair stream (weak scaling) instead of a shard of one")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pgo", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=192, help="pairs in the CPU baseline sample")
-    p.add_argument("--cpu-workers", type=int, default=16)
+    p.add_argument("--cpu-workers", type=int, default=0, help="0 = every core this job may use")
     p.add_argument("--instance", type=int, default=-1, help="force a kernel instance (diagnostics)")
     p.add_argument("--sched-probe", type=int, default=-1,
                    help="phase-1 iterations of the batch scheduler (0 = one launch; -1 = library default)")
@@ -82,15 +84,10 @@ def init_dist(args):
     return world, rank, local
 
 
-def sd_shard_per(n, world):
-    from slamhip import dist as sd
-    return sd.shard_range(n, world, 0)[2]
-
-
 def make_workload(args, world, rank):
     from slamhip import se2, synthetic
     from slamhip import dist as sd
-    if args.strong:
+    if not args.weak:
         total = args.pairs
         lo, hi, _ = sd.shard_range(total, world, rank)
         seq = synthetic.make_sequence(total + 1, seed=2025, n_beams=args.beams)
@@ -104,32 +101,117 @@ def make_workload(args, world, rank):
     return scans, inits
 
 
-def cpu_baseline(scans, inits, sample, workers):
-    """NumPy port of the reference (per-query loop of src/icp.py:16-17, same
-    arithmetic as the reference), fanned out with joblib loky like
-    scripts/main.py:240 — on `workers` host cores."""
+def host_cpu():
+    """(logical CPUs of the machine, CPUs this process may use, model name)."""
+    n_all = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n_aff = n_all
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n_all, n_aff, model
+
+
+def default_cpu_workers():
+    """All host cores this job may use (scripts/main.py:240 uses n_jobs=-1):
+    the affinity set, capped by OMP_NUM_THREADS where the launcher sets the
+    job's CPU share (the GPU box: 16 per GPU, while os.cpu_count() shows the
+    whole machine)."""
+    _, n_aff, _ = host_cpu()
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n_aff, int(cap))) if cap and cap.isdigit() else n_aff
+
+
+def _oracle_pair(pc1, pc2, init, loop):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    from joblib import Parallel, delayed
     import icp_oracle
+    fn = icp_oracle.correspondences_loop if loop else icp_oracle.correspondences
+    h, e = icp_oracle.icp(pc1, pc2, init, 0.05, 100, corr_fn=fn)
+    return h[-1], float(e), len(h) - 1
 
-    def one(pc1, pc2, init):
-        h, e = icp_oracle.icp(pc1, pc2, init, 0.05, 100, corr_fn=icp_oracle.correspondences_loop)
-        return len(h) - 1
 
-    idx = np.linspace(0, len(inits) - 1, sample).astype(int)
-    jobs = [(np.c_[scans[i + 1], np.ones(len(scans[i + 1]))], np.c_[scans[i], np.ones(len(scans[i]))],
-             inits[i].copy()) for i in idx]
+def cpu_baseline(scans, inits, sample, workers):
+    """The reference's ICP restated in NumPy (oracle/icp_oracle.py, bit-exact
+    with src/icp.py) on this host's cores, on bounded samples of this workload:
+
+      ref_loop   the reference's per-query loop (src/icp.py:16-17)
+      vectorized the same arithmetic over query blocks (bit-identical results)
+
+    each on 1 core and on `workers` cores through joblib loky, as
+    scripts/main.py:240 fans icp() out.  `value` is ref_loop on all cores
+    (what scripts/main.py runs).  Returns (baseline dict, {pair index: (tf,
+    err, iters)} of the all-core ref_loop sample) — the second feeds the
+    parity block."""
+    from joblib import Parallel, delayed
     env = {"OMP_NUM_THREADS": "1", "OPENBLAS_NUM_THREADS": "1", "MKL_NUM_THREADS": "1"}
+    saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
-    par = Parallel(n_jobs=workers, backend="loky")
-    par(delayed(one)(*jobs[0]) for _ in range(min(workers, 4)))   # spin the pool up
-    t0 = time.perf_counter()
-    its = par(delayed(one)(*j) for j in jobs)
-    dt = time.perf_counter() - t0
-    return {"value": round(sample / dt, 3), "unit": "scan-pairs/s", "cores": workers, "kind": "port",
-            "sample": f"{sample} pairs of this workload (1081-pt scans, mean {np.mean(its):.1f} ICP iterations), "
-                      f"oracle/icp_oracle.py with the reference's per-query loop, joblib loky x{workers} "
-                      f"(scripts/main.py:240 pattern), {dt:.1f} s wall"}
+    n_all, n_aff, model = host_cpu()
+
+    def job(i):
+        return (np.c_[scans[i + 1], np.ones(len(scans[i + 1]))], np.c_[scans[i], np.ones(len(scans[i]))],
+                inits[i].copy())
+
+    def run(idx, loop, n_jobs):
+        t0 = time.perf_counter()
+        if n_jobs == 1:
+            out = [_oracle_pair(*job(i), loop) for i in idx]
+        else:
+            out = par(delayed(_oracle_pair)(*job(i), loop) for i in idx)
+        return out, time.perf_counter() - t0
+
+    try:
+        par = Parallel(n_jobs=workers, backend="loky")
+        par(delayed(_oracle_pair)(*job(0), False) for _ in range(workers))   # spin the pool up
+        modes = {}
+        idx_all = np.linspace(0, len(inits) - 1, sample).astype(int)
+        res_all, dt = run(idx_all, True, workers)
+        modes["ref_loop_all_cores"] = {"pairs": len(idx_all), "s": round(dt, 2), "pairs_per_s": round(len(idx_all) / dt, 3)}
+        n1 = max(2, sample // (2 * workers))
+        idx1 = idx_all[:n1]
+        _, dt = run(idx1, True, 1)
+        modes["ref_loop_1_core"] = {"pairs": n1, "s": round(dt, 2), "pairs_per_s": round(n1 / dt, 3)}
+        nv = max(4, sample // 12)
+        idxv = idx_all[:nv]
+        _, dt = run(idxv, False, 1)
+        modes["vectorized_1_core"] = {"pairs": nv, "s": round(dt, 2), "pairs_per_s": round(nv / dt, 3)}
+        _, dt = run(idx_all, False, workers)
+        modes["vectorized_all_cores"] = {"pairs": len(idx_all), "s": round(dt, 2),
+                                         "pairs_per_s": round(len(idx_all) / dt, 3)}
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    its = [r[2] for r in res_all]
+    base = {"value": modes["ref_loop_all_cores"]["pairs_per_s"], "unit": "scan-pairs/s", "cores": workers,
+            "kind": "port",
+            "sample": f"{len(idx_all)} evenly spaced pairs of this workload (1081-pt scans, mean {np.mean(its):.1f} "
+                      f"ICP iterations): oracle/icp_oracle.py with the reference's per-query loop "
+                      f"(src/icp.py:16-17), joblib loky x{workers} (scripts/main.py:240 pattern)",
+            "modes": modes, "host": {"os_cpu_count": n_all, "affinity_cpus": n_aff, "workers": workers,
+                                     "cpu_model": model}}
+    return base, {int(i): r for i, r in zip(idx_all, res_all)}
+
+
+def parity_block(res, ref):
+    """GPU results of the timed launches vs the CPU port on the sampled pairs."""
+    idx = sorted(ref)
+    dtf = max(float(np.abs(res.tf[i] - ref[i][0]).max()) for i in idx)
+    derr = max(abs(float(res.err[i]) - ref[i][1]) / max(1.0, abs(ref[i][1])) for i in idx)
+    eq = all(int(res.iters[i]) == ref[i][2] for i in idx)
+    return {"pairs": len(idx), "max_abs_tf_diff": dtf, "max_rel_err_diff": derr, "iters_equal": eq,
+            "tolerance": 1e-9, "ok": bool(eq and dtf <= 1e-9 and derr <= 1e-9),
+            "reference": "oracle/icp_oracle.py (bit-exact restatement of src/icp.py)"}
 
 
 def pgo_bench():
@@ -209,36 +291,24 @@ def main():
     lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)
+    from slamhip import dist as sd
     gathered = None
-    Bpad = max(B, 1)
     if world > 1:
-        if args.strong:
-            Bpad = max(sd_shard_per(args.pairs, world), 1)
-        gathered = torch.empty((world, Bpad, 11), dtype=torch.float64, device=ss.device)
-        local_res = torch.zeros((Bpad, 11), dtype=torch.float64, device=ss.device)
+        # SE(2) edge + error + iteration count of every pair, padded to the shard size
+        Bpad = max(sd.shard_range(args.pairs, world, 0)[2] if not args.weak else B, 1)
+        gathered = torch.empty((world, Bpad, sd.RESULT_WIDTH), dtype=torch.float64, device=ss.device)
+        local_res = torch.zeros((Bpad, sd.RESULT_WIDTH), dtype=torch.float64, device=ss.device)
 
     stream = torch.cuda.current_stream()
 
-    from slamhip import dist as sd
-
-    def pack_results(buf):
-        # SE(2) edges + error + iteration count of every pair, padded to Bpad rows
-        sd.pack(batch.out_tf[:B], batch.out_err[:B], batch.out_iters[:B], Bpad, out=buf)
-
     def exchange():
-        if args.dist_backend == "nccl":
-            dist.all_gather_into_tensor(gathered, local_res)
-        else:   # gloo dry run: host staging
-            parts = [torch.empty_like(local_res, device="cpu") for _ in range(world)]
-            dist.all_gather(parts, local_res.cpu())
-            gathered.copy_(torch.stack(parts))
+        sd.pack(batch.out_tf[:B], batch.out_err[:B], batch.out_iters[:B], Bpad, out=local_res)
+        sd.all_gather_results(local_res, out=gathered)
 
     def step():
         batch.launch()
         if world > 1:
-            # SE(2) edges + error + iteration count of every pair -> every rank
-            pack_results(local_res)
-            exchange()
+            exchange()   # SE(2) edges of every pair -> every rank
 
     for _ in range(args.warmup):
         step()
@@ -253,7 +323,6 @@ def main():
         batch.launch()
         ev[i][1].record(stream)
         if world > 1:
-            pack_results(local_res)
             exchange()
     torch.cuda.synchronize()
     if world > 1:
@@ -323,7 +392,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8(d) ray-cast room, 1081 beams/270 deg, 0.01 m noise; EECS_3 unavailable offline)",
@@ -354,9 +423,19 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(scans, inits, args.cpu_sample, args.cpu_workers)
+            workers = args.cpu_workers or default_cpu_workers()
+            out["cpu_baseline"], ref = cpu_baseline(scans, inits, args.cpu_sample, workers)
+            out["parity"] = parity_block(res, ref)
         except Exception as e:   # keep the GPU line even if the host pool fails
             out["cpu_baseline"] = {"error": repr(e)}
+    if "parity" not in out:
+        # no CPU baseline run (N > 1 or --no-cpu-baseline): a small vectorised sample
+        idx = np.linspace(0, B - 1, min(B, 6)).astype(int) if B else []
+        ref = {int(i): _oracle_pair(np.c_[scans[i + 1], np.ones(len(scans[i + 1]))],
+                                    np.c_[scans[i], np.ones(len(scans[i]))], inits[i].copy(), False) for i in idx}
+        if ref:
+            out["parity"] = parity_block(res, ref)
+            out["parity"]["scope"] = "rank 0's shard"
     if world == 1 and not args.no_pgo:
         try:
             out["pgo"] = pgo_bench()

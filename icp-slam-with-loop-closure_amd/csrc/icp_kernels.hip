@@ -35,7 +35,9 @@
 
 namespace slamhip {
 
-constexpr int kCandCap = 4096;          // pc2 points resident in LDS (64 KiB fp64 + 32 KiB fp32)
+constexpr int kCandCap = 4096;
+constexpr int32_t kBadBounds = INT32_MIN;   // out_iters of a pair outside the launch's bounds
+__device__ int g_icp_status;                // nonzero: some pair was outside its launch's bounds          // pc2 points resident in LDS (64 KiB fp64 + 32 KiB fp32)
 constexpr int kRedDoubles = 2 * 8 * 9;   // two reduction slabs, <= 8 waves x 9
 
 struct IcpArgs {
@@ -181,25 +183,6 @@ __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf
 // rows 0-1 and 2-3, v_permlane32_swap the two halves).  Every lane returns the
 // result.
 #define SLAM_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
-#ifndef SLAM_PERMLANE
-#define SLAM_PERMLANE 1
-#endif
-#if !SLAM_PERMLANE   // A/B reference: the four row results through SGPRs
-__device__ __forceinline__ float cross_rows_min(float v) {
-    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-    return fminf(fminf(r0, r1), fminf(r2, r3));
-}
-__device__ __forceinline__ float cross_rows_max(float v) {
-    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
-}
-#else
 __device__ __forceinline__ float cross_rows_min(float v) {
     const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     v = fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
@@ -212,7 +195,6 @@ __device__ __forceinline__ float cross_rows_max(float v) {
     const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
 }
-#endif
 __device__ __forceinline__ float wave_min_f(float v) {
     v = fminf(v, SLAM_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
     v = fminf(v, SLAM_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
@@ -271,36 +253,10 @@ __device__ __forceinline__ float box_lb(f32x2 alo, f32x2 ahi, const float4& b) {
 // Skipped candidates have d32 >= lower bound > M2 at the time of the test, and
 // M2 only decreases, so (M1, M2, J1) equal the full scan's.
 constexpr int kSub = 8;
-#ifndef SLAM_WIN
-#define SLAM_WIN 4
-#endif
-#ifndef SLAM_PREFETCH
-#define SLAM_PREFETCH 1   // winners and matches of all groups loaded at once (A/B: 0)
-#endif
-#ifndef SLAM_STAGE_UNROLL
-#define SLAM_STAGE_UNROLL 4
-#endif
-#ifndef SLAM_SHIFT
-#define SLAM_SHIFT 1
-#endif
-#ifndef SLAM_ABLATE
-#define SLAM_ABLATE 0   // diagnostics only (tools/ab_fixed.py): 1 no visits, 2 no certification, 4 no block sums, 8 no clearance
-#endif
-#ifndef SLAM_KEEPQ
-#define SLAM_KEEPQ 0
-#endif
-constexpr int kWin = SLAM_WIN;
-#ifndef SLAM_BATCH
-#define SLAM_BATCH 3
-#endif
-constexpr int kBatch = SLAM_BATCH;   // live sub-chunks tested per batch
-// waves/SIMD the default 1081-point instances are compiled for (A/B builds override)
-#ifndef SLAM_WPE
-#define SLAM_WPE 4
-#endif
-#ifndef SLAM_WPE320
-#define SLAM_WPE320 1
-#endif
+constexpr int kWin = 4;          // window sub-chunks (32 candidates); 2/5/6/8 measured slower
+constexpr int kStageUnroll = 4;  // staging loads in flight per thread
+constexpr int kBatch = 3;        // live sub-chunks tested per batch
+constexpr int kWpe = 4;          // waves/SIMD the default 1081-point instance is compiled for
 
 // Screened distances are non-negative (or +inf), so their IEEE bit patterns
 // order like unsigned integers: the updates run on the bits (integer min /
@@ -387,7 +343,6 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         const int wp = st_ws(st[k]);
         const int sh = ws[k] - wp;
         float rl = st_radius(st[k]);
-#if SLAM_SHIFT
         if (sh != 0) {
             const int c0 = sh > 0 ? wp : wp + kWin - 1;          // sub-chunks that left the window
             const int c1 = sh > 0 ? wp + 1 : wp + kWin - 2;
@@ -398,17 +353,8 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             rl = fminf(rl, sqrtf(lb) * (1.0f - 1e-5f));
         }
         const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2[k];
-#else
-        const bool settled = sh == 0 && rl * rl * (1.0f - 1e-5f) > M2[k];
-#endif
         act[k] = valid[k] && !settled;
         if (settled && sh != 0) st[k] = st_pack(rl, ws[k]);
-#if SLAM_ABLATE & 1
-        act[k] = false;
-#endif
-#if SLAM_ABLATE & 8
-        act[k] = valid[k];
-#endif
     }
     lap(1);
     // 3. per group with active queries: the box of the active fp32 queries and
@@ -428,20 +374,13 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
         const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
         float gf = INFINITY, lmin = INFINITY;
-#if SLAM_ABLATE & 32
-        for (int w = 0; w < 0; ++w) {
-#else
         for (int w = 0; w < nw; ++w) {
-#endif
             const int sl = 64 * w + lane;
             // branch-free (no short-circuit): the LDS reads are not serialised behind exec-mask jumps
             const float glb = box_lb(f32x2{bx0, by0}, f32x2{bx1, by1}, box8[min(sl, nsub - 1)]);
             const bool gl = glb <= gM2;
             gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
             uint64_t live = __ballot((sl < nsub) & gl);
-#if SLAM_ABLATE & 16
-            live = 0;
-#endif
             if (stamping) tsub[3] += __popcll(live);
             while (live) {
                 // up to kBatch live sub-chunks per batch, straight-line: the box
@@ -531,7 +470,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     int it0 = 0;
     if (a.resume) {
         const int s = a.out_iters[b];
-        if (s > 0) return;   // uniform: the whole workgroup leaves
+        if (s > 0 || s == kBadBounds) return;   // uniform: the whole workgroup leaves
         it0 = -s;
     }
     const int s1 = a.src_scan[b];
@@ -543,10 +482,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     const double2* __restrict__ p1 = a.pts + o1;
     const double2* __restrict__ p2 = a.pts + o2;
     const bool resident = n2 <= cap;
+    // the caller's bounds (max_n1 / max_n2) chose this instance and the LDS
+    // size: a pair outside them would be computed wrongly, so it is flagged
+    // instead (slam_icp_status returns SLAM_EINVAL) and left undone
+    if (n1 < 1 || n2 < 1 || n1 > BLOCK * QPT || (SCREEN && !resident)) {
+        if (tid == 0) {
+            if (!STEP) a.out_iters[b] = kBadBounds;
+            a.out_err[b] = __builtin_nan("");
+            atomicOr(&g_icp_status, 1);
+        }
+        return;   // uniform
+    }
 
     double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound)
     if (resident) {
-#pragma unroll SLAM_STAGE_UNROLL
+#pragma unroll kStageUnroll
         for (int j = tid; j < n2; j += BLOCK) {   // unrolled: several loads in flight per thread
             const double2 p = p2[j];
             cand[j] = p;
@@ -588,7 +538,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     if constexpr (SCREEN) {
         double cm[2] = {cmax, 0.0};
         if constexpr (PRUNE) {
-#pragma unroll SLAM_STAGE_UNROLL
+#pragma unroll kStageUnroll
             for (int i = tid; i < n1; i += BLOCK) {
                 const double2 p = p1[i];
                 cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));
@@ -680,10 +630,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     const double ty = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
                     fx[k] = static_cast<float>(tx);
                     fy[k] = static_cast<float>(ty);
-#if SLAM_KEEPQ
-                    qx[k] = tx;
-                    qy[k] = ty;
-#endif
                     if constexpr (PRUNE) {
                         // carried clearance minus this iteration's motion of the fp32
                         // query: |q_t - q_{t-1}| <= |dT p| + fp32 rounding of both
@@ -724,7 +670,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 }
                 stamp(0);
                 // ---- certify: the screened winner is the exact fp64 argmin? ---
-#if SLAM_PREFETCH
                 // the winners' fp64 coordinates for every group at once: one LDS
                 // latency instead of one per (divergent) certification branch
                 double2 cw[QPT];
@@ -732,11 +677,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 #pragma unroll
                     for (int k = 0; k < QPT; ++k) cw[k] = cand[min(C1[k], n2 - 1)];
                 }
-#endif
 #pragma unroll
                 for (int k = 0; k < QPT; ++k) {
                     const int i = k * BLOCK + tid;
-#if !SLAM_KEEPQ
                     double x = 0.0, y = 0.0;
                     if (i < n1) {
                         const double2 p = p1[i];
@@ -745,7 +688,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     }
                     qx[k] = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));   // bit-identical to above
                     qy[k] = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
-#endif
                     // winning chunk: first index reaching the chunk minimum + runner-up
                     float b2 = INFINITY;
                     int j1 = C1[k];
@@ -766,19 +708,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     if (!screen) {
                         ok = i >= n1;   // |coordinates| >= 1e18: every query takes the exact path
                     } else if (i < n1 && n2 > 1) {
-#if SLAM_PREFETCH
                         const double2 c = PRUNE ? cw[k] : cand[j1];
-#else
-                        const double2 c = cand[j1];
-#endif
                         const double d1 = exact_d2(c.x, c.y, qx[k], qy[k]);
                         const double s2 = static_cast<double>(fminf(M2[k], b2));   // every other j: d32 >= s2
                         const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
                         const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
                         ok = cq < 1e18 && s2 < 3.0e38 && certify(d1, s2, ab);
-#if SLAM_ABLATE & 2
-                        ok = true;
-#endif
                     }
                     // wave-cooperative exact fp64 scan for each uncertified query of
                     // this group: the whole wave scans pc2 for it, a (distance, index)
@@ -856,20 +791,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 
         // ---- src/icp.py:64,68  centroids + error ------------------------------
         double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-#if SLAM_PREFETCH
         double2 mk[QPT];   // matched points of every group at once (one memory latency)
 #pragma unroll
         for (int k = 0; k < QPT; ++k) mk[k] = resident ? cand[bi[k]] : p2[bi[k]];
-#endif
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
             const int i = k * BLOCK + tid;
             if (i < n1) {
-#if SLAM_PREFETCH
                 const double2 m = mk[k];
-#else
-                const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
-#endif
                 v[0] += qx[k];
                 v[1] += qy[k];
                 v[2] += m.x;
@@ -877,9 +806,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 v[4] += exact_d2(m.x, m.y, qx[k], qy[k]);   // (pc1_t - pc2[corr])**2 of the row
             }
         }
-#if !(SLAM_ABLATE & 4)
         block_sum<5, WAVES>(v, red0);
-#endif
         const double n = static_cast<double>(n1);
         const double mux = v[0] / n, muy = v[1] / n;     // pc1_avg
         const double mvx = v[2] / n, mvy = v[3] / n;     // pc2_avg
@@ -900,12 +827,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 s[3] = fma(ya, yb, s[3]);
             }
         }
-#if !(SLAM_ABLATE & 4)
         block_sum<4, WAVES>(s, red1);
-#else
-        s[0] = uniform_d(s[0]); s[1] = uniform_d(s[1]); s[2] = uniform_d(s[2]); s[3] = uniform_d(s[3]);
-        v[0] = uniform_d(v[0]); v[1] = uniform_d(v[1]); v[2] = uniform_d(v[2]); v[3] = uniform_d(v[3]); v[4] = uniform_d(v[4]);
-#endif
 
         // ---- closed-form 2x2 Kabsch: R maximising tr(R S) ---------------------
         // Equals V diag(1, det(V U^T)) U^T of the reference's SVD route.
@@ -1019,7 +941,7 @@ struct Instance {
 static const Instance kInstances[] = {
     SLAM_INST(64, 1, 1),   SLAM_INST(64, 2, 1),   SLAM_INST(64, 4, 1),   SLAM_INST(128, 3, 1),
     SLAM_INST(128, 4, 1),  SLAM_INST(192, 4, 1),  SLAM_INST(192, 6, 1),  SLAM_INST(256, 4, 1),
-    SLAM_INST(256, 5, SLAM_WPE), SLAM_INST(320, 4, SLAM_WPE320),  SLAM_INST(384, 3, 1),  SLAM_INST(512, 3, 1),
+    SLAM_INST(256, 5, kWpe), SLAM_INST(320, 4, 1),  SLAM_INST(384, 3, 1),  SLAM_INST(512, 3, 1),
     SLAM_INST(576, 2, 1),  SLAM_INST(512, 4, 1),  SLAM_INST(512, 6, 1),  SLAM_INST(512, 8, 1),
     SLAM_INST(512, 16, 1),
 };
@@ -1258,6 +1180,22 @@ int slam_icp_set_schedule(int probe_iters, int min_pairs) {
     g_sched_min_pairs = min_pairs;
     return ok();
 }
+// Bounds check of every ICP launch since the last call: synchronises `stream`
+// and returns SLAM_EINVAL if a pair's scans were empty or outside the
+// max_n1 / max_n2 the caller passed (that pair's out_iters = INT32_MIN, its
+// out_err NaN), then clears the flag.
+int slam_icp_status(void* stream) {
+    if (hipStreamSynchronize(as_stream(stream)) != hipSuccess) return fail(SLAM_EHIP, "icp status: stream sync");
+    int st = 0;
+    if (hipMemcpyFromSymbol(&st, HIP_SYMBOL(g_icp_status), sizeof(int)) != hipSuccess)
+        return fail(SLAM_EHIP, "icp status: read");
+    if (st == 0) return ok();
+    const int zero = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_icp_status), &zero, sizeof(int));
+    return fail(SLAM_EINVAL, "icp: a pair's scan sizes exceed the max_n1 / max_n2 bounds of its launch "
+                             "(or a scan is empty); its out_iters is INT32_MIN");
+}
+
 int slam_icp_set_screen(int mode) {
     if (mode < 0 || mode > 2) return fail(SLAM_EINVAL, "nn mode %d not in {0, 1, 2}", mode);
     g_screen = mode;

@@ -57,12 +57,6 @@ __device__ __forceinline__ M3 m3_transpose(const M3& x) {
 
 // Inverse by LU with partial pivoting (dgesv on the identity), enough for the
 // well-conditioned R sigma R^T blocks here.
-#ifndef SLAM_SGD_FASTMOD
-#define SLAM_SGD_FASTMOD 1
-#endif
-#ifndef SLAM_SGD_FAST
-#define SLAM_SGD_FAST 1   // relaxation chain: closed-form inverse, reciprocal total weights (A/B: 0)
-#endif
 __device__ __forceinline__ M3 m3_inv(const M3& m) {
     double A[3][3], X[3][3];
 #pragma unroll
@@ -143,17 +137,6 @@ __device__ __forceinline__ M3 diag3(double v) {
 
 __device__ __forceinline__ bool is_loop_edge(int a, int b) { return a - b != 1 && b - a != 1; }
 
-// NumPy float remainder (npy_divmod): fmod, then shift into the divisor's sign.
-__device__ __forceinline__ double py_mod(double x, double m) {
-    double r = fmod(x, m);
-    if (r != 0.0) {
-        if ((m < 0.0) != (r < 0.0)) r += m;
-    } else {
-        r = copysign(0.0, m);
-    }
-    return r;
-}
-
 // x mod 2 pi into [0, 2 pi) (Python's float %) without fmod's remainder loop:
 // one floor, one fma and a one-step correction (agrees with the exact
 // remainder to ~1e-16 |x|; tests at 1e-9).
@@ -201,19 +184,22 @@ __global__ void sgd_gamma_kernel(const int32_t* __restrict__ ea, const int32_t* 
 }
 
 // M[i][j] in edge order; also 1/M for the relaxation pass.  One thread / node.
-__global__ void sgd_weights_kernel(int32_t N, const int32_t* __restrict__ ea,
-                                   const int32_t* __restrict__ eb, int32_t E,
+// Only loop edges with a < b cover any node (a < i <= b), i.e. exactly the
+// compacted active list (sgd_compact_kernel, networkx order kept), so each
+// node sums over K edges instead of all E, in the same order.
+__global__ void sgd_weights_kernel(int32_t N, const int32_t* __restrict__ A, const int32_t* __restrict__ B,
+                                   const int32_t* __restrict__ IDX, const int32_t* __restrict__ Kp,
                                    const double* __restrict__ dw, double* __restrict__ invM) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
+    const int K = *Kp;
     double m0 = 0.0, m1 = 0.0, m2 = 0.0;
-    for (int e = 0; e < E; ++e) {
-        const int a = ea[e], b = eb[e];
-        if (!is_loop_edge(a, b)) continue;
-        if (a < i && i <= b) {
-            m0 = m0 + dw[3 * e + 0];
-            m1 = m1 + dw[3 * e + 1];
-            m2 = m2 + dw[3 * e + 2];
+    for (int k = 0; k < K; ++k) {
+        if (A[k] < i && i <= B[k]) {
+            const double* w = dw + 3 * static_cast<int64_t>(IDX[k]);
+            m0 = m0 + w[0];
+            m1 = m1 + w[1];
+            m2 = m2 + w[2];
         }
     }
     invM[3 * i + 0] = 1.0 / m0;
@@ -277,7 +263,8 @@ __global__ __launch_bounds__(1024) void sgd_compact_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ eb,
                                                            const double* __restrict__ tf, int32_t E,
                                                            int32_t* __restrict__ A, int32_t* __restrict__ B,
-                                                           double* __restrict__ TF, int32_t* __restrict__ K) {
+                                                           double* __restrict__ TF, int32_t* __restrict__ IDX,
+                                                           int32_t* __restrict__ K) {
     __shared__ int wcount[16];
     __shared__ int base;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -303,6 +290,7 @@ __global__ __launch_bounds__(1024) void sgd_compact_kernel(const int32_t* __rest
             const int k = off + pos_w;
             A[k] = a;
             B[k] = b;
+            IDX[k] = e;
 #pragma unroll
             for (int q = 0; q < 9; ++q) TF[9 * static_cast<int64_t>(k) + q] = tf[9 * static_cast<int64_t>(e) + q];
         }
@@ -355,9 +343,6 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
     }
     __syncthreads();
 
-#if !SLAM_SGD_FASTMOD
-    const double TWO_PI = 2.0 * M_PI;
-#endif
     double alpha[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -419,17 +404,9 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
         double r[3];
         r[0] = Pb.a[0][2] - pb[0];
         r[1] = Pb.a[1][2] - pb[1];
-#if SLAM_SGD_FASTMOD
         r[2] = py_mod_2pi(atan2(Pb.a[1][0], Pb.a[0][0]) - pb[2]);
-#else
-        r[2] = py_mod(atan2(Pb.a[1][0], Pb.a[0][0]) - pb[2], TWO_PI);
-#endif
-#if SLAM_SGD_FAST
         const M3 Wi = m3_inv_adj(m3_mul(m3_mul(m3_transpose(R), S), R));
-#else
-        const M3 Wi = m3_inv(m3_mul(m3_mul(m3_transpose(R), S), R));
-#endif
-        double beta[3], rtw[3];
+        double beta[3];
         const int L = b - a;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -438,8 +415,12 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             double bj = (static_cast<double>(L) * dj) * alpha[j];
             if (fabs(bj) > fabs(r[j])) bj = r[j];
             beta[j] = bj;
-            rtw[j] = cur.cb[j] - cur.ca[j];           // total_weight over (a, b]
         }
+        // Every thread read P[a] and P[b] above, and node b is one of this
+        // edge's explicit nodes: no thread may write it before all have read
+        // it.  The residual chain above sits between the reads and this
+        // barrier, so the waves arrive together and it is cheap.
+        __syncthreads();
         // ---- explicit nodes (a's block remainder, b's block) ----------------------
         {
             int i = cur.ni;
@@ -448,11 +429,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             while (i >= 0) {
                 if (i <= b) {
 #pragma unroll
-#if SLAM_SGD_FAST
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) * cur.irtw[j]);
-#else
-                    for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) / rtw[j]);
-#endif
                 } else {
 #pragma unroll
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
@@ -472,11 +449,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             if (q < bb) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
-#if SLAM_SGD_FAST
                     const double g = beta[j] * cur.irtw[j];
-#else
-                    const double g = beta[j] / rtw[j];
-#endif
                     cA[3 * q + j] += g;
                     off[3 * q + j] -= g * cur.ca[j];
                 }
@@ -538,9 +511,9 @@ using namespace slamhip;
 extern "C" {
 
 int64_t slam_pgo_sgd_work_size(int32_t N, int32_t E) {
-    // invM (3N) | dw (3E) | gamma (4) | C (3N+3) | TF (9E) | A, B (E int32 each) | K
+    // doubles: invM (3N) | dw (3E) | gamma (4) | C (3N+3) | TF (9E) | then int32: A, B, IDX (E each) | K
     return 3 * static_cast<int64_t>(N) + 3 * static_cast<int64_t>(E) + 4 + 3 * (static_cast<int64_t>(N) + 1) +
-           9 * static_cast<int64_t>(E) + static_cast<int64_t>(E) + 1;
+           9 * static_cast<int64_t>(E) + (3 * static_cast<int64_t>(E) + 2) / 2;
 }
 
 int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb,
@@ -557,14 +530,15 @@ int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int
     double* TF = C + 3 * (static_cast<int64_t>(N) + 1);
     int32_t* A = reinterpret_cast<int32_t*>(TF + 9 * static_cast<int64_t>(E));
     int32_t* Bv = A + E;
-    int32_t* Kp = Bv + E;
+    int32_t* IDX = Bv + E;
+    int32_t* Kp = IDX + E;
     hipLaunchKernelGGL(sgd_dw_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, E,
                        loop_closure_uncertainty, dw);
     hipLaunchKernelGGL(sgd_gamma_kernel, dim3(1), dim3(64), 0, s, ea, eb, E, dw, gamma);
-    hipLaunchKernelGGL(sgd_weights_kernel, dim3((N + 127) / 128), dim3(128), 0, s, N, ea, eb, E, dw,
+    hipLaunchKernelGGL(sgd_compact_kernel, dim3(1), dim3(1024), 0, s, ea, eb, tf, E, A, Bv, TF, IDX, Kp);
+    hipLaunchKernelGGL(sgd_weights_kernel, dim3((N + 127) / 128), dim3(128), 0, s, N, A, Bv, IDX, Kp, dw,
                        invM);
     hipLaunchKernelGGL(sgd_prefix_kernel, dim3(1), dim3(kRelaxBlock), 0, s, invM, N, C);
-    hipLaunchKernelGGL(sgd_compact_kernel, dim3(1), dim3(1024), 0, s, ea, eb, tf, E, A, Bv, TF, Kp);
     // lazy-offset block size 2^sh: >= 64 nodes, at most kMaxOffBlocks blocks
     int sh = 6;
     while ((((N - 1) >> sh) + 1) > kMaxOffBlocks) ++sh;
@@ -576,6 +550,9 @@ int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int
         hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxBlock), lds, s, poses, N, A, Bv, TF,
                            Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
     } else {
+        // off + cA reach 2 x 3 x 2048 doubles (96 KiB): above the 64 KiB default
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(offb));
         hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxBlock), offb, s, poses, N, A, Bv,
                            TF, Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
     }

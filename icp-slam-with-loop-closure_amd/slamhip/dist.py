@@ -32,17 +32,41 @@ def pack(tf, err, iters, rows, out=None):
     return out
 
 
-def all_gather_results(local, group=None):
-    """(rows, 11) per rank -> (world, rows, 11) on every rank."""
+def all_gather_results(local, group=None, out=None):
+    """(rows, 11) per rank -> (world, rows, 11) on every rank: ONE
+    all_gather_into_tensor over RCCL ("nccl" backend); with gloo (CPU tests,
+    dry runs) the rows go through host tensors."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+    if out is None:
+        out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "gloo":
-        dist.all_gather(list(out.unbind(0)), local, group=group)
+        parts = [torch.empty(tuple(local.shape), dtype=local.dtype) for _ in range(world)]
+        dist.all_gather(parts, local.cpu(), group=group)
+        out.copy_(torch.stack(parts))
     else:
         dist.all_gather_into_tensor(out, local, group=group)
     return out
+
+
+def sharded_chain(odometry0, tf_local, n_items, group=None, iters_local=None, err_local=None):
+    """Every rank's ICP edges of its contiguous shard -> the full odometry chain
+    (scripts/main.py:249-256) on every rank.  Returns (poses (n+1, 3), tf, err, iters)."""
+    import torch
+    import torch.distributed as dist
+    from . import se2
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi, per = shard_range(n_items, world, rank)
+    B = hi - lo
+    tf = torch.as_tensor(np.asarray(tf_local, dtype=np.float64).reshape(B, 9))
+    err = torch.as_tensor(np.zeros(B) if err_local is None else np.asarray(err_local, dtype=np.float64))
+    its = torch.as_tensor(np.zeros(B, np.int64) if iters_local is None else np.asarray(iters_local))
+    local = pack(tf, err, its, max(per, 1))
+    g = all_gather_results(local, group)
+    tf_all, err_all, it_all = unpack(g, n_items)
+    return se2.compose_chain(np.asarray(odometry0, dtype=np.float64), tf_all), tf_all, err_all, it_all
 
 
 def unpack(gathered, n_items):

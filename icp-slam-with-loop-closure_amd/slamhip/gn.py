@@ -121,6 +121,17 @@ class GaussNewton:
         captured once into a HIP graph and replayed (``graph=False`` forces
         eager launches)."""
         t = dv.torch()
+        if tol is not None and iterations > 1:
+            # early exit: one step at a time, stop once chi2 (before each step)
+            # changes by less than tol relative to the previous one
+            out = []
+            for _ in range(iterations):
+                out.append(float(self.run(1, None, stream, graph)[0]))
+                if len(out) > 1 and abs(out[-2] - out[-1]) <= tol * max(abs(out[-2]), 1e-300):
+                    break
+            self.chi2 = np.asarray(out)
+            return self.chi2
+        self.status.zero_()   # a failed earlier run must not poison this one
         if graph is None:
             graph = self._eager_done and stream is None and iterations > 0
         if graph:

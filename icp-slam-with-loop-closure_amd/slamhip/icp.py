@@ -109,8 +109,14 @@ class IcpBatch:
             dv.ptr(self.out_tf), dv.ptr(self.out_err), dv.ptr(self.out_iters), dv.stream_handle(stream)),
             "slam_icp_batch_f64")
 
+    def check(self, stream=None):
+        """Synchronise and raise if the kernel flagged a pair outside the launch bounds."""
+        _abi.check(_abi.lib().slam_icp_status(dv.stream_handle(stream)), "slam_icp_batch_f64")
+
     def result(self):
         B = self.B
+        if B:
+            self.check()
         tf = self.out_tf[:B].cpu().numpy().reshape(B, 3, 3)
         err = self.out_err[:B].cpu().numpy()
         iters = self.out_iters[:B].cpu().numpy().astype(np.int64)
@@ -163,6 +169,7 @@ def icp_step(scans, src, dst, T_in, rotation_only=False, device=None, stream=Non
         dv.ptr(ss.pts), dv.ptr(ss.scan_off), dv.ptr(d_src), dv.ptr(d_dst), dv.ptr(d_T), B,
         int(bool(rotation_only)), int(n1.max()), int(ss.lens[dst].max()), dv.ptr(T_out), dv.ptr(corr),
         dv.ptr(d_off), dv.ptr(err), dv.stream_handle(stream)), "slam_icp_step_f64")
+    _abi.check(L.slam_icp_status(dv.stream_handle(stream)), "slam_icp_step_f64")
     c = corr.cpu().numpy()
     corr_list = [c[corr_off[b]:corr_off[b] + n1[b]] for b in range(B)]
     return T_out.cpu().numpy().reshape(B, 3, 3), corr_list, err.cpu().numpy()

@@ -27,14 +27,21 @@ class PoseGraph():
         """
         self.poses = poses
         self.graph = nx.DiGraph()
+        # new (not pickled): node a's heading when the constructor wrote the
+        # global-frame delta of edge (a, a+1) — what optimize_pose_graph needs
+        # to re-express that edge in node a's frame for Gauss-Newton
+        self.odometry_headings = {}
         if poses is None:
             return
         deltas = np.diff(poses, axis=0)
         self.graph.add_edges_from((i, i + 1, {"object": odom_change_to_mat(d)}) for i, d in enumerate(deltas))
+        self.odometry_headings = {i: float(poses[i, 2]) for i in range(len(deltas))}
 
     def add_constraint(self, i, j, transformation):
         """Adds (or overwrites, keeping its position) the edge i -> j."""
         self.graph.add_edge(i, j, object=transformation)
+        if j == i + 1:
+            self.odometry_headings.pop(i, None)   # no longer the constructor's global delta
 
     def flip(self):
         """Reverse node order (theta + pi) and remap every edge a->b to
@@ -42,6 +49,7 @@ class PoseGraph():
         self.poses = self.poses[::-1]
         self.poses[:, 2] = (self.poses[:, 2] + np.pi) % (2 * np.pi)
         last = len(self.poses) - 1
+        self.odometry_headings = {}   # flipped edges are no longer constructor deltas
         flipped = nx.DiGraph()
         flipped.add_edges_from((last - b, last - a, {"object": t}) for a, b, t in self.graph.edges(data="object"))
         self.graph = flipped
@@ -54,6 +62,7 @@ class PoseGraph():
         # Only for pose graphs this pipeline wrote itself (pickle executes code).
         with open(fname, "rb") as f:
             self.poses, self.graph = pickle.load(f)
+        self.odometry_headings = {}   # unknown after a load: see optimize_pose_graph
 
     def export_g2o(self, fname):
         rows = ["VERTEX_SE2 %d %f %f %f" % (i, p[0], p[1], p[2]) for i, p in enumerate(self.poses)]

@@ -48,16 +48,57 @@ def construct_R(pose_graph, idx):
 
 
 def optimize_pose_graph(pose_graph, iterations=10, odom_information=2.0, loop_information=5.0,
-                        tol=1e-9, return_history=False):
+                        tol=None, return_history=False, odometry_edges="global_delta", loop_edges="icp"):
     """Gauss-Newton on the SE(2) graph (relative-pose residuals, information
     2 I for odometry edges and 5 I for loop edges as ``PoseGraph.export_g2o``
-    writes them); node 0 is held fixed.  Updates ``pose_graph.poses`` in place."""
+    writes them); node 0 is held fixed.  Updates ``pose_graph.poses`` in place.
+
+    GN measures every edge a -> b as z with X_b = X_a z.  The graph as
+    scripts/main.py builds it holds two other conventions, converted here
+    (``gn_measurements``): the constructor's odometry edges (b = a + 1) are
+    GLOBAL-frame deltas P[a+1] - P[a] (reference src/pose_graph.py:32-36) and
+    are re-expressed in node a's frame (``odometry_edges="global_delta"``;
+    ``"relative"`` keeps them); loop edges are ICP results T of
+    icp(pc_a, pc_b), i.e. X_a = X_b T (scripts/main.py:305), so z = T^-1
+    (``loop_edges="icp"``; ``"relative"`` keeps them).  ``tol`` stops early
+    once chi2 changes by less than tol (relative) between iterations."""
     from slamhip import gn as _gn
-    ea, eb, tf = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
+    ea, eb, tf = gn_measurements(pose_graph, odometry_edges, loop_edges)
     solver = _gn.GaussNewton(pose_graph.poses, ea, eb, tf, odom_information, loop_information)
-    hist = solver.run(iterations, tol)
+    hist = solver.run(iterations, tol=tol)
     pose_graph.poses[...] = solver.host_poses()
     return hist if return_history else None
+
+
+def gn_measurements(pose_graph, odometry_edges="global_delta", loop_edges="icp"):
+    """(ea, eb, z (E, 3, 3)) in networkx edge order with X_b = X_a z for every edge.
+
+    A constructor odometry edge (a, a+1) holds odom_change_to_mat(P[a+1] - P[a]):
+    rotation by the heading change and the GLOBAL translation delta; its
+    relative measurement is R(theta_a)^T delta with theta_a the heading the
+    delta was taken at (``PoseGraph.odometry_headings``; the current pose's
+    heading for graphs without it, e.g. loaded from a pickle before
+    optimisation, as scripts/main.py saves them)."""
+    if odometry_edges not in ("global_delta", "relative") or loop_edges not in ("icp", "relative"):
+        raise ValueError("odometry_edges in {global_delta, relative}, loop_edges in {icp, relative}")
+    ea, eb, tf = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
+    z = np.array(tf, dtype=np.float64).reshape(-1, 3, 3)
+    odo = eb.astype(np.int64) == ea.astype(np.int64) + 1
+    if odometry_edges == "global_delta" and odo.any():
+        known = getattr(pose_graph, "odometry_headings", {}) or {}
+        th = np.array([known.get(int(a), pose_graph.poses[int(a), 2]) for a in ea[odo]], dtype=np.float64)
+        c, s = np.cos(th), np.sin(th)
+        dx, dy = z[odo, 0, 2].copy(), z[odo, 1, 2].copy()
+        z[odo, 0, 2] = c * dx + s * dy
+        z[odo, 1, 2] = -s * dx + c * dy
+    if loop_edges == "icp" and (~odo).any():
+        r = z[~odo]
+        inv = np.zeros_like(r)
+        inv[:, :2, :2] = np.transpose(r[:, :2, :2], (0, 2, 1))        # R^T
+        inv[:, :2, 2] = -np.einsum("eij,ej->ei", inv[:, :2, :2], r[:, :2, 2])
+        inv[:, 2, 2] = 1.0
+        z[~odo] = inv
+    return ea, eb, z
 
 
 def _edges(pose_graph):

@@ -17,8 +17,11 @@
  *     (np.c_[points, ones] as scripts/main.py:242-243 builds them);
  *   - 3x3 SE(2) matrices are 9 float64, row-major, last row [0, 0, 1];
  *   - launches are asynchronous and ordered on `stream` (a hipStream_t; NULL
- *     = the legacy default stream); nothing is allocated, nothing is copied to
- *     the host, so every call can be captured into a hipGraph;
+ *     = the legacy default stream) and copy nothing to the host; nothing is
+ *     allocated persistently.  One exception to "allocates nothing": a
+ *     slam_icp_batch_f64 call of >= 2048 pairs takes a transient
+ *     stream-ordered workspace (hipMallocAsync / hipFreeAsync, 12 B per pair),
+ *     which stream capture records as graph memory nodes;
  *   - return 0 on success, a negative SLAM_E* code on failure; the message is
  *     available from slam_last_error() (thread-local).
  */
@@ -56,8 +59,11 @@ int slam_icp_max_query_points(void);
  *   dst_scan  int32[B]  pc2 (reference cloud) of pair b
  *   init      float64[B][9] initial transforms
  *   max_n1/max_n2  host upper bounds of the pc1 / pc2 sizes in this batch
- *                  (select the kernel instance and LDS size; not checked
- *                  against the data beyond n1 <= slam_icp_max_query_points())
+ *                  (select the kernel instance and LDS size).  The kernel
+ *                  checks every pair against them: a pair with an empty scan
+ *                  or n1 > max_n1's instance capacity or n2 > max_n2's LDS
+ *                  capacity is not computed (out_iters = INT32_MIN, out_err =
+ *                  NaN) and raises the flag slam_icp_status() reports
  *   hist_stride    0, or >= max_iters + 3: out_hist[b] holds the full
  *                  transform list [init, T1, ..., T_k] the reference returns
  *   out_hist  float64[B][hist_stride][9] (NULL if hist_stride == 0)
@@ -76,6 +82,14 @@ int slam_icp_batch_f64(const double* pts, const int64_t* scan_off,
                        int32_t rotation_only, int32_t max_n1, int32_t max_n2,
                        int32_t hist_stride, double* out_hist, double* out_tf,
                        double* out_err, int32_t* out_iters, void* stream);
+
+/*
+ * Synchronises `stream` and reports the device-side bounds check of every
+ * slam_icp_batch_f64 / slam_icp_step_f64 launch since the previous call:
+ * SLAM_OK, or SLAM_EINVAL when some pair was outside its launch's max_n1 /
+ * max_n2 (see above); the flag is then cleared.
+ */
+int slam_icp_status(void* stream);
 
 /*
  * One ICP iteration per pair.  Replaces src/icp.py:55-69 `icp_iteration(pc1,

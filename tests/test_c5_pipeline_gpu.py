@@ -1,0 +1,71 @@
+"""Config C5 in shape (BASELINE.json configs[4]: "Full pipeline: synthetic
+indoor loop, batched ICP + loop-closure re-optimisation, map vs CPU
+reference") through the batched driver, checked stage by stage against the
+reference's flow (scripts/main.py:236-339) restated with the CPU oracle:
+
+* stage 1: per-pair icp() (init = pose_to_mat(odom_i - odom_{i-1})) + chain;
+* stage 2: manual loop closures (identity init, accepted when err < 30);
+* stage 3: 50 SGD steps (lr = 1/(k+1)) + the orientation recompute;
+* the final occupancy map of a subset of scans vs oracle/occupancy_oracle.
+
+3,000 scans of 181 beams keep the oracle's flow within about a minute (the
+full 50k x 1081 run is tools/c5_pipeline.py; same code path, larger arrays).
+Positions within 1e-9, headings within 1e-9 (compared raw, not modulo 2 pi:
+the orientation recompute leaves atan2-range headings), map cells equal.
+"""
+import numpy as np
+import pytest
+
+from conftest import homog
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+def test_c5_shape_pipeline_vs_oracle():
+    import icp_oracle
+    import occupancy_oracle as oo
+    import pgo_oracle as po
+    import src.pose_graph as pgm
+    import src.produce_occupancy_grid as pog
+    from slamhip import pipeline, se2, synthetic
+    s = synthetic.make_loop_sequence(3000, seed=9, n_beams=181)
+    assert len(s.loop_pairs) >= 20
+
+    # ---- GPU: the batched driver -------------------------------------------
+    r = pipeline.scan_matching(s.odometry, s.scans)
+    pg = pgm.PoseGraph(r.poses.copy())
+    ok = pipeline.manual_loop_closures(pg, s.scans, s.loop_pairs)
+    pipeline.optimize(pg, s.scans, optimization_max_iters=50)
+    sub = np.arange(0, len(s.scans), 60)
+    grid, origin = pog.produce_occupancy_grid(pg.poses[sub], [s.scans[i] for i in sub], 0.05)
+
+    # ---- oracle: the reference's flow ----------------------------------------
+    tfs = []
+    for i in range(1, len(s.scans)):
+        h, _ = icp_oracle.icp(homog(s.scans[i]), homog(s.scans[i - 1]),
+                              se2.pose_to_mat(s.odometry[i] - s.odometry[i - 1]), 0.05, 100)
+        tfs.append(h[-1])
+    chain = se2.compose_chain(s.odometry[0], np.stack(tfs))
+    assert np.abs(r.poses[:, :2] - chain[:, :2]).max() <= TOL
+    assert np.abs(r.poses[:, 2] - chain[:, 2]).max() <= TOL
+    ref_pg = pgm.PoseGraph(chain.copy())
+    acc = []
+    for i, j in s.loop_pairs:
+        h, e = icp_oracle.icp(homog(s.scans[i]), homog(s.scans[j]), np.eye(3), 0.05, 100)
+        acc.append(e < 30)
+        if e < 30:
+            ref_pg.add_constraint(int(i), int(j), h[-1])
+    assert ok.tolist() == acc and ok.mean() > 0.8
+    ea, eb, tf = ref_pg.edge_arrays()
+    ga, gb, gtf = pg.edge_arrays()
+    assert np.array_equal(ea, ga) and np.array_equal(eb, gb) and np.abs(tf - gtf).max() <= TOL
+    ref = chain.copy()
+    for k in range(50):
+        ref = po.sgd_step(ref, ea, eb, tf, learning_rate=1 / float(k + 1))
+    ref = po.orient_from_positions(ref)
+    assert np.abs(pg.poses[:, :2] - ref[:, :2]).max() <= TOL
+    assert np.abs(pg.poses[:, 2] - ref[:, 2]).max() <= TOL
+    # the map kernel on the same (already checked) poses
+    rgrid, rorigin = oo.produce(pg.poses[sub], [s.scans[i] for i in sub], 0.05)
+    assert origin == rorigin and np.array_equal(grid, rgrid)

@@ -133,7 +133,8 @@ def test_gn_wide_band_global_window():
 @pytest.mark.gpu
 def test_optimize_pose_graph_dropin():
     """src.pose_graph_optimization.optimize_pose_graph on a reference-style
-    PoseGraph (odometry edges from PoseGraph.__init__, identity loop edges)."""
+    PoseGraph (odometry edges from PoseGraph.__init__, identity loop edges):
+    the GPU solve of the converted measurements equals the oracle's."""
     import src.pose_graph as pgm
     import src.pose_graph_optimization as pgo
     from slamhip import synthetic
@@ -141,7 +142,7 @@ def test_optimize_pose_graph_dropin():
     pg = pgm.PoseGraph(poses.copy())
     for a, b in loops:
         pg.add_constraint(a, b, np.eye(3))
-    ea, eb, tf = pg.edge_arrays()
+    ea, eb, tf = pgo.gn_measurements(pg)      # constructor deltas -> node frames; loop edges inverted
     ref, ref_chi = go.optimize(poses.copy(), ea, eb, tf, iterations=3)
     obj = pg.poses
     chis = pgo.optimize_pose_graph(pg, iterations=3, return_history=True)
@@ -201,3 +202,79 @@ def test_gn_graph_replay_matches_eager():
     chi_g = np.concatenate([b.run(1, graph=False), b.run(3, graph=True)])
     assert np.array_equal(chi_e, chi_g)
     assert np.array_equal(a.host_poses(), b.host_poses())
+
+
+def test_oracle_jacobians_match_finite_differences():
+    """The GN oracle's analytic Jacobians A = de/dx_a, B = de/dx_b against
+    central differences of its own residual (self-consistency of the oracle)."""
+    guess, ea, eb, tf = _random_graph(30, 20, 7)
+    z = go.edge_measurements(tf)
+    w = go.information(ea, eb)
+    e0, A, B = go.linearize(guess, ea, eb, z, w)
+    h = 1e-6
+    for side, J in ((ea, A), (eb, B)):
+        for c in range(3):
+            num = np.zeros_like(e0)
+            for sgn in (1, -1):
+                p = guess.copy()
+                # perturb node side[e] of every edge separately: one edge at a time
+                for e in range(len(ea)):
+                    q = guess.copy()
+                    q[side[e], c] += sgn * h
+                    ee, _, _ = go.linearize(q, ea[e:e + 1], eb[e:e + 1], z[e:e + 1], w[e:e + 1])
+                    num[e] += sgn * ee[0]
+            num /= 2 * h
+            self_loop = ea == eb
+            assert np.abs(num[~self_loop] - J[~self_loop, :, c]).max() < 1e-6
+
+
+def test_gn_measurements_of_a_consistent_graph_have_zero_chi2():
+    """PoseGraph(poses) + exact ICP-convention loop edges (X_a = X_b T): after
+    optimize_pose_graph's conversion every residual vanishes at the initial
+    poses, so GN would leave them unchanged (CPU: the oracle's chi2)."""
+    import src.pose_graph as pgm
+    import src.pose_graph_optimization as pgo
+    from slamhip import se2, synthetic
+    s = synthetic.make_loop_sequence(400, seed=3, n_beams=31)
+    pg = pgm.PoseGraph(s.truth.copy())
+    for a, b in s.loop_pairs:
+        T = np.linalg.inv(se2.pose_to_mat(s.truth[b])) @ se2.pose_to_mat(s.truth[a])   # X_a = X_b T
+        pg.add_constraint(int(a), int(b), T)
+    ea, eb, z = pgo.gn_measurements(pg)
+    _, _, _, chi2 = go.build_system(s.truth.copy(), ea.astype(np.int64), eb.astype(np.int64),
+                                    go.edge_measurements(z), go.information(ea, eb))
+    assert chi2 < 1e-20
+    # the raw (unconverted) edges are NOT consistent once headings turn
+    ra, rb, rtf = pg.edge_arrays()
+    _, _, _, chi2_raw = go.build_system(s.truth.copy(), ra.astype(np.int64), rb.astype(np.int64),
+                                        go.edge_measurements(rtf), go.information(ra, rb))
+    assert chi2_raw > 1.0
+    # after a pickle round trip the headings come from the saved poses: same z
+    q = pgm.PoseGraph(None)
+    q.poses, q.graph = pg.poses, pg.graph
+    assert np.allclose(pgo.gn_measurements(q)[2], z, atol=1e-15)
+
+
+@pytest.mark.gpu
+def test_pipeline_gn_reduces_drift():
+    """The batched driver's GN path (scan matching -> PoseGraph -> manual loop
+    closures -> optimize(method="gn")) on a loop sequence: the optimised
+    trajectory is closer to the ground truth than the ICP chain, and GN on the
+    unchanged chain graph (no loop edges) leaves it where it is."""
+    import src.pose_graph as pgm
+    from slamhip import pipeline, synthetic
+    s = synthetic.make_loop_sequence(1200, seed=6)
+    r = pipeline.scan_matching(s.odometry, s.scans)
+    # no loop edges: the converted odometry edges are consistent -> no motion
+    pg0 = pgm.PoseGraph(r.poses.copy())
+    chis = __import__("src.pose_graph_optimization", fromlist=["x"]).optimize_pose_graph(
+        pg0, iterations=2, return_history=True)
+    assert chis[0] < 1e-12 and np.abs(pg0.poses[:, :2] - r.poses[:, :2]).max() < 1e-9
+    pg = pgm.PoseGraph(r.poses.copy())
+    ok = pipeline.manual_loop_closures(pg, s.scans, s.loop_pairs)
+    assert ok.mean() > 0.8
+    pipeline.optimize(pg, s.scans, method="gn", gn_iterations=5)
+
+    def ate(p):   # position error after aligning the first pose (the chain starts at odometry[0])
+        return float(np.sqrt(np.mean(np.sum((p[:, :2] - s.truth[:, :2]) ** 2, axis=1))))
+    assert ate(pg.poses) < 0.7 * ate(r.poses)

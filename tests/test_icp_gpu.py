@@ -359,3 +359,42 @@ def test_default_schedule_large_batch(k):
     assert phased.iters.max() > 5
     assert np.array_equal(phased.iters, single.iters)
     assert np.array_equal(phased.tf, single.tf) and np.array_equal(phased.err, single.err)
+
+
+def test_default_schedule_c3_shape_vs_oracle(k, oracle):
+    """The benchmarked path itself: 2,400 consecutive pairs of 1081-point scans
+    (the C3 stream generator, seed 2025) through the DEFAULT two-phase
+    scheduler; a strided sample plus the longest-running pairs against the
+    CPU oracle (scripts/main.py:240-247 parameters): iteration counts equal,
+    transforms within 1e-9, errors within 1e-9 relative."""
+    n = 2400
+    seq, inits = _sequence_pairs(n, seed=2025)
+    assert min(len(s) for s in seq.scans) > 1000
+    res = k.icp_batch(seq.scans, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
+    sample = sorted(set(range(0, n, 200)) | set(np.argsort(res.iters)[-4:].tolist()))
+    assert res.iters.max() > 30          # the long tail reaches deep into phase 2
+    for b in sample:
+        h, e = oracle.icp(homog(seq.scans[b + 1]), homog(seq.scans[b]), inits[b].copy(), 0.05, 100)
+        assert res.iters[b] == len(h) - 1, b
+        assert np.abs(res.tf[b] - h[-1]).max() <= TOL, b
+        assert abs(res.err[b] - e) <= TOL * max(1.0, e), b
+
+
+def test_understated_bounds_are_flagged(k):
+    """A raw C caller that passes max_n1 / max_n2 below the real scan sizes
+    gets SLAM_EINVAL from slam_icp_status (the offending pairs are not
+    computed), not silently wrong results; correct bounds then work again."""
+    from slamhip import _abi
+    n = 6
+    seq, inits = _sequence_pairs(n, seed=3, n_beams=361)
+    ss = k.ScanSet(seq.scans)
+    for attr, val in (("max_n2", 200), ("max_n1", 100)):
+        b = k.IcpBatch(ss, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
+        setattr(b, attr, val)
+        b.launch()
+        with pytest.raises(_abi.SlamHipError, match="bounds"):
+            b.result()
+        assert (b.out_iters[:n].cpu().numpy() == np.iinfo(np.int32).min).all()
+    good = k.IcpBatch(ss, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
+    good.launch()
+    assert (good.result().iters > 0).all()

@@ -83,3 +83,27 @@ def test_sgd_large_graph_vs_oracle():
     got = pgo.sgd_step(poses, ea, eb, tf, learning_rate=1.0)
     assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-7
     assert np.abs(_wrap(got[:, 2] - ref[:, 2])).max() <= 1e-7
+
+
+@pytest.mark.parametrize("pps,laps,ncons", [(150, 15, 3000), (875, 40, 250)])
+def test_sgd_global_memory_path_vs_oracle(pps, laps, ncons):
+    """Graphs above the LDS pose capacity (N > 6,144 -> sgd_relax_kernel<false>):
+    9,000 nodes, and 140,000 nodes where the lazy-offset blocks grow past 64
+    nodes (sh > 6, 96 KiB of dynamic LDS).  Three steps vs the oracle."""
+    import pgo_oracle as po
+    from slamhip import pgo, synthetic
+    poses, loops = synthetic.lap_pose_graph(side_len=3.0, poses_per_side=pps, num_loops=laps, seed=1,
+                                            num_constraints=ncons)
+    assert len(poses) > 6144
+    pg = _graph(poses, [], [], [])
+    for a, b in loops:
+        pg.add_constraint(a, b, np.eye(3))
+    ea, eb, tf = pg.edge_arrays()
+    ref = poses.copy()
+    s = pgo.SgdSolver(poses, ea, eb, tf)
+    for k in range(3):
+        po.sgd_step(ref, ea, eb, tf, learning_rate=1.0 / (k + 1))
+        s.step(1.0 / (k + 1))
+    got = s.host_poses()
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-7
+    assert np.abs(got[:, 2] - ref[:, 2]).max() <= 1e-9 * max(1.0, np.abs(ref[:, 2]).max())

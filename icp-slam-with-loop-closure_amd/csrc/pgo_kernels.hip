@@ -330,9 +330,11 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
     double* off = reinterpret_cast<double*>(smem);                // [nblk][3] lazy offsets
     double* cA = off + 3 * nblk;                                  // [nblk][3] lazy ramp coefficients
     double* P = IN_LDS ? cA + 3 * nblk : g_poses;
+    __shared__ uint32_t rd_count;   // waves done reading P[a], P[b] (all edges so far)
     const int tid = threadIdx.x;
     const int K = *Kp;
     const int bs = 1 << sh;
+    if (tid == 0) rd_count = 0;
 
     for (int i = tid; i < 3 * nblk; i += kRelaxBlock) {
         off[i] = 0.0;
@@ -417,16 +419,22 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             beta[j] = bj;
         }
         // Every thread read P[a] and P[b] above, and node b is one of this
-        // edge's explicit nodes: no thread may write it before all have read
-        // it.  The residual chain above sits between the reads and this
-        // barrier, so the waves arrive together and it is cheap.
-        __syncthreads();
+        // edge's explicit nodes: its owner may not write it before every wave
+        // has read it.  Each wave counts itself in after its residual chain
+        // (which consumed the reads); only the owner of b waits for the count
+        // (normally already complete), the other threads go on.
+        if ((tid & 63) == 0) __hip_atomic_fetch_add(&rd_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t rd_target = static_cast<uint32_t>(kRelaxBlock / 64) * static_cast<uint32_t>(k + 1);
         // ---- explicit nodes (a's block remainder, b's block) ----------------------
         {
             int i = cur.ni;
             int t = tid;
             double cij[3] = {cur.ci[0], cur.ci[1], cur.ci[2]};
             while (i >= 0) {
+                if (i == b) {
+                    while (__hip_atomic_load(&rd_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < rd_target)
+                        __builtin_amdgcn_s_sleep(1);
+                }
                 if (i <= b) {
 #pragma unroll
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) * cur.irtw[j]);

@@ -124,12 +124,21 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
         for (int k = 0; k < NV; ++k) red[wave * NV + k] = v[k];
     }
     __syncthreads();
+    if constexpr (WAVES <= 8) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        double s = red[k];
+        for (int k = 0; k < NV; ++k) {
+            double s = red[k];
 #pragma unroll
-        for (int w = 1; w < WAVES; ++w) s += red[w * NV + k];
-        v[k] = s;
+            for (int w = 1; w < WAVES; ++w) s += red[w * NV + k];
+            v[k] = s;
+        }
+    } else {
+        // 16-wave workgroups: lane w reads wave w's partials and the wave sums
+        // them with the DPP tree (fixed order; NV registers instead of WAVES*NV)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = lane < WAVES ? red[lane * NV + k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = readlane_d(wave_sum(v[k]), 0);
     }
 }
 

@@ -38,7 +38,8 @@ namespace slamhip {
 constexpr int kCandCap = 4096;
 constexpr int32_t kBadBounds = INT32_MIN;   // out_iters of a pair outside the launch's bounds
 __device__ int g_icp_status;                // nonzero: some pair was outside its launch's bounds          // pc2 points resident in LDS (64 KiB fp64 + 32 KiB fp32)
-constexpr int kRedDoubles = 2 * 8 * 9;   // two reduction slabs, <= 8 waves x 9
+// two reduction slabs of 8 doubles per wave at the front of the dynamic LDS
+__host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 8; }
 
 struct IcpArgs {
     const double2* pts;
@@ -283,14 +284,16 @@ __device__ __forceinline__ uint32_t st_pack(float r, int ws) {
     return (__float_as_uint(r) & ~kWsMask) | static_cast<uint32_t>(ws);
 }
 
-template <int QPT>
+// NQ <= QPT: the wave's groups k >= NQ hold no query (k * BLOCK + 64 * wave >=
+// n1, e.g. group 4 of waves 1-3 for 1081-point scans at 256x5) and are skipped.
+template <int QPT, int NQ>
 __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ candf,
                                                  const float4* __restrict__ box8, int nsub,
                                                  const float (&qx)[QPT], const float (&qy)[QPT],
                                                  const bool (&valid)[QPT], const int (&pred)[QPT],
                                                  uint32_t (&st)[QPT],
                                                  float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
-                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[5],
+                                                 int& nvisit, bool stamping, unsigned long long (&tsub)[9],
                                                  bool counting, unsigned long long& nev) {
     const int lane = threadIdx.x & 63;
     unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
@@ -315,7 +318,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 #pragma unroll 2
     for (int t = 0; t < kWin * kSub; t += 2) {
 #pragma unroll
-        for (int k = 0; k < QPT; ++k) {
+        for (int k = 0; k < NQ; ++k) {
             const float4 pp = *reinterpret_cast<const float4*>(candf + ws[k] * kSub + t);
             const f32x2v d = screen_pair(pp, qx[k], qy[k]);
             take_cand(d.x, t, M1[k], M2[k], J1[k]);
@@ -339,7 +342,9 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     //    window to the next iteration.
     bool act[QPT];
 #pragma unroll
-    for (int k = 0; k < QPT; ++k) {
+    for (int k = NQ; k < QPT; ++k) act[k] = false;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
         const int wp = st_ws(st[k]);
         const int sh = ws[k] - wp;
         float rl = st_radius(st[k]);
@@ -368,12 +373,21 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
         if (__ballot(act[k]) == 0) continue;   // wave-uniform
+        unsigned long long f0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
+        auto flap = [&](int q) {   // diagnostics: group-loop sub-phases (workgroup 0, wave 0)
+            if (stamping) {
+                const unsigned long long f1 = __builtin_amdgcn_s_memtime();
+                tsub[q] += f1 - f0;
+                f0 = f1;
+            }
+        };
         const float bx0 = wave_min_f(act[k] ? qx[k] : INFINITY);
         const float bx1 = wave_max_f(act[k] ? qx[k] : -INFINITY);
         const float by0 = wave_min_f(act[k] ? qy[k] : INFINITY);
         const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
         const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
         float gf = INFINITY, lmin = INFINITY;
+        flap(5);
         for (int w = 0; w < nw; ++w) {
             const int sl = 64 * w + lane;
             // branch-free (no short-circuit): the LDS reads are not serialised behind exec-mask jumps
@@ -382,6 +396,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
             uint64_t live = __ballot((sl < nsub) & gl);
             if (stamping) tsub[3] += __popcll(live);
+            flap(6);
             while (live) {
                 // up to kBatch live sub-chunks per batch, straight-line: the box
                 // reads (broadcast) and tests issue back to back
@@ -409,6 +424,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                 need &= has;
                 // scan the sub-chunks some lane needs (rolled loop: small code)
                 uint32_t todo = wave_or_u32(need);
+                flap(7);
                 while (todo) {
                     const int u = __builtin_ctz(todo);
                     todo &= todo - 1;
@@ -425,6 +441,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                         }
                     }
                 }
+                flap(8);
             }
         }
         // lb <= d32 <= (1 + 5u) |q - p|^2, so |q - p| >= sqrt(lb) (1 - 1e-5)
@@ -448,13 +465,16 @@ __device__ __forceinline__ bool certify(double d1, double s2, double a) {
     return s2 > fc;
 }
 
-template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false, int WPE = 1>
+// DIAG: a diagnostics build of the kernel (per-phase s_memtime stamps of
+// workgroup 0, in-kernel candidate-evaluation counter); the product kernels
+// are compiled without any of it.
+template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false, int WPE = 1, bool DIAG = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void icp_kernel(IcpArgs a) {
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* red0 = reinterpret_cast<double*>(smem);
     double* red1 = red0 + WAVES * 8;
-    double2* cand = reinterpret_cast<double2*>(smem + kRedDoubles * sizeof(double));
+    double2* cand = reinterpret_cast<double2*>(smem + red_doubles(BLOCK) * sizeof(double));
     const int cap = a.cand_cap;
     // SCREEN only: fp32 copy of the candidates and per-wave fallback queues
     float2* candf = reinterpret_cast<float2*>(cand + cap);
@@ -584,10 +604,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     double last_err = it0 > 0 ? a.out_err[b] : 0.0;
     __syncthreads();
 
-    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[5] = {0, 0, 0, 0, 0};
+    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
-    const bool stamping = a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
-    const bool counting = a.evals != nullptr;
+    const bool stamping = DIAG && a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
+    const bool counting = DIAG && a.evals != nullptr;
     unsigned long long nev = 0;
     auto stamp = [&](int ph) {
         if (stamping) {
@@ -600,7 +620,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         if (stamping && lane == 0) {
             for (int q = 0; q < 4; ++q) a.stamps[q] = tph[q];
             a.stamps[4] = static_cast<unsigned long long>(nscan_total);   // sub-chunks visited (wave 0)
-            for (int q = 0; q < 5; ++q) a.stamps[5 + q] = tsub[q];
+            for (int q = 0; q < 9; ++q) a.stamps[5 + q] = tsub[q];
         }
     };
     stamp(-1);
@@ -657,8 +677,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                                                     : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
                             vq[k] = i < n1;
                         }
-                        nn_window_pruned<QPT>(candf, box8, nsub, fx, fy, vq, pred, st, M1, M2, C1,
-                                              nscan_total, stamping, tsub, counting, nev);
+                        // groups holding queries (uniform; only the last can be empty)
+                        const int nq = min(QPT, (n1 - 64 * wave + BLOCK - 1) / BLOCK);
+                        if (QPT > 1 && nq == QPT - 1)
+                            nn_window_pruned<QPT, (QPT > 1 ? QPT - 1 : QPT)>(candf, box8, nsub, fx, fy, vq, pred,
+                                                                               st, M1, M2, C1, nscan_total,
+                                                                               stamping, tsub, counting, nev);
+                        else
+                            nn_window_pruned<QPT, QPT>(candf, box8, nsub, fx, fy, vq, pred, st, M1, M2, C1,
+                                                       nscan_total, stamping, tsub, counting, nev);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
                         if (counting) {   // full screen + winning-chunk rescan
@@ -930,6 +957,7 @@ struct Instance {
     KernelFn step_screen;
     KernelFn batch_prune;    // fp32 screen with exact chunk pruning (default)
     KernelFn step_prune;
+    KernelFn batch_prune_diag;   // the same with stamps / evaluation counter (diagnostics)
 };
 
 // W: minimum waves per SIMD the pruned batch kernel is compiled for (4 on the
@@ -937,7 +965,8 @@ struct Instance {
 #define SLAM_INST(B, Q, W)                                                                 \
     {B, Q, icp_kernel<B, Q, false, false>, icp_kernel<B, Q, true, false>,                 \
      icp_kernel<B, Q, false, true>, icp_kernel<B, Q, true, true>,                         \
-     icp_kernel<B, Q, false, true, true, W>, icp_kernel<B, Q, true, true, true>}
+     icp_kernel<B, Q, false, true, true, W>, icp_kernel<B, Q, true, true, true>,        \
+     icp_kernel<B, Q, false, true, true, W, true>}
 static const Instance kInstances[] = {
     SLAM_INST(64, 1, 1),   SLAM_INST(64, 2, 1),   SLAM_INST(64, 4, 1),   SLAM_INST(128, 3, 1),
     SLAM_INST(128, 4, 1),  SLAM_INST(192, 4, 1),  SLAM_INST(192, 6, 1),  SLAM_INST(256, 4, 1),
@@ -1040,12 +1069,13 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     a.evals = g_icp_evals;
     a.cand_cap = max_n2 < kCandCap ? ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk : kCandCap;
     const int mode = max_n2 <= kCandCap ? g_screen : 0;
-    size_t lds = kRedDoubles * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
+    size_t lds = red_doubles(inst->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
     if (mode >= 1)
         lds += static_cast<size_t>(a.cand_cap) * sizeof(float2);
     if (mode == 2)
         lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4);
-    KernelFn fn = mode == 2 ? (step ? inst->step_prune : inst->batch_prune)
+    const bool diag = (a.stamps || a.evals) && mode == 2 && !step;   // diagnostics: pruned batch only
+    KernelFn fn = mode == 2 ? (step ? inst->step_prune : (diag ? inst->batch_prune_diag : inst->batch_prune))
                 : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)
                             : (step ? inst->step : inst->batch);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -209,7 +209,9 @@ int slam_gn_set_solver(int mode);
 int slam_gn_bcr_block_rows(int32_t nv, int32_t W);
 int slam_icp_set_stamps(void* dev_buf);
 /* Count candidate-distance evaluations performed (all lanes) into a device
- * uint64 (atomic add per wave); NULL turns counting off. */
+ * uint64 (atomic add per wave); NULL turns counting off.  Stamps and the
+ * counter run in a separate diagnostics build of the pruned batch kernel
+ * (NN mode 2, slam_icp_batch_f64 only); the product kernels carry neither. */
 int slam_icp_set_eval_counter(void* dev_u64);
 
 #ifdef __cplusplus

@@ -1,0 +1,62 @@
+"""Latency of ONE ICP pair alone on the GPU (the strong-scaling tail), per
+kernel instance, plus per-phase s_memtime stamps.  GPU only.
+
+    python tools/lone_pair.py [pair ...]      (default: the longest C3 pairs)
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+import torch  # noqa: E402
+from slamhip import _abi, se2, synthetic  # noqa: E402
+from slamhip import icp as k  # noqa: E402
+
+pairs = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or [1118, 7264, 0]
+trunc = next((int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--n1=")), 0)   # diagnostics: pc1 prefix
+seq = synthetic.make_sequence(max(pairs) + 2, seed=2025)
+lib = _abi.lib()
+if trunc:
+    seq.scans = [s[:trunc] if i - 1 in pairs else s for i, s in enumerate(seq.scans)]
+shapes = {}
+for i in range(lib.slam_icp_num_instances()):
+    b, q = ctypes.c_int32(), ctypes.c_int32()
+    lib.slam_icp_instance_shape(i, ctypes.byref(b), ctypes.byref(q))
+    if b.value * q.value >= (trunc or 1081):
+        shapes[i] = f"{b.value}x{q.value}"
+ss = k.ScanSet(seq.scans)
+for p in pairs:
+    init = se2.pose_to_mat(seq.odometry[p + 1] - seq.odometry[p])[None]
+    batch = k.IcpBatch(ss, [p + 1], [p], init, epsilon=0.05, max_iters=100)
+    line = []
+    for i, name in shapes.items():
+        lib.slam_icp_force_instance(i)
+        batch.launch()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(7):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            batch.launch()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        its = int(batch.result().iters[0])
+        line.append(f"{name}:{np.median(ts) * 1e3 / its:.1f}")
+    lib.slam_icp_force_instance(-1)
+    print(f"pair {p} iters {its} us/iter " + " ".join(line), flush=True)
+    buf = torch.zeros(16, dtype=torch.int64, device="cuda")
+    lib.slam_icp_set_stamps(buf.data_ptr())
+    batch2 = k.IcpBatch(ss, [p + 1], [p], init, epsilon=0.05, max_iters=100)
+    batch2.launch()
+    torch.cuda.synchronize()
+    lib.slam_icp_set_stamps(None)
+    t = buf.cpu().numpy().astype(float) / its
+    print(f"   stamps/iter (wave 0): scan {t[0]:.0f} certify {t[1]:.0f} fallback {t[2]:.0f} reduce+kabsch {t[3]:.0f} "
+          f"| window {t[5]:.0f} mask {t[6]:.0f} visits {t[7]:.0f} | visited sub-chunks/iter {t[4]:.1f} "
+          f"live/iter {t[8]:.1f} batches/iter {t[9]:.1f}", flush=True)
+    print(f"   group loop/iter: box reductions {t[10]:.0f} group mask {t[11]:.0f} tests+or {t[12]:.0f} scans {t[13]:.0f}",
+          flush=True)

@@ -36,6 +36,7 @@
 namespace slamhip {
 
 constexpr int kCandCap = 4096;
+constexpr size_t kMaxLds = 160 * 1024;      // LDS per workgroup (gfx950)
 constexpr int32_t kBadBounds = INT32_MIN;   // out_iters of a pair outside the launch's bounds
 __device__ int g_icp_status;                // nonzero: some pair was outside its launch's bounds          // pc2 points resident in LDS (64 KiB fp64 + 32 KiB fp32)
 // two reduction slabs of 8 doubles per wave at the front of the dynamic LDS
@@ -291,7 +292,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                                                  const float4* __restrict__ box8, int nsub,
                                                  const float (&qx)[QPT], const float (&qy)[QPT],
                                                  const bool (&valid)[QPT], const int (&pred)[QPT],
-                                                 uint32_t (&st)[QPT],
+                                                 uint32_t* __restrict__ st, int st_stride,
                                                  float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
                                                  int& nvisit, bool stamping, unsigned long long (&tsub)[9],
                                                  bool counting, unsigned long long& nev) {
@@ -345,9 +346,10 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     for (int k = NQ; k < QPT; ++k) act[k] = false;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-        const int wp = st_ws(st[k]);
+        const uint32_t stk = st[k * st_stride];   // LDS: not held in registers across the window scan
+        const int wp = st_ws(stk);
         const int sh = ws[k] - wp;
-        float rl = st_radius(st[k]);
+        float rl = st_radius(stk);
         if (sh != 0) {
             const int c0 = sh > 0 ? wp : wp + kWin - 1;          // sub-chunks that left the window
             const int c1 = sh > 0 ? wp + 1 : wp + kWin - 2;
@@ -359,7 +361,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         }
         const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2[k];
         act[k] = valid[k] && !settled;
-        if (settled && sh != 0) st[k] = st_pack(rl, ws[k]);
+        if (settled && sh != 0) st[k * st_stride] = st_pack(rl, ws[k]);
     }
     lap(1);
     // 3. per group with active queries: the box of the active fp32 queries and
@@ -446,7 +448,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         }
         // lb <= d32 <= (1 + 5u) |q - p|^2, so |q - p| >= sqrt(lb) (1 - 1e-5)
         const float gfar = wave_min_f(gf);
-        if (act[k]) st[k] = st_pack(sqrtf(fminf(gfar, lmin)) * (1.0f - 1e-5f), ws[k]);
+        if (act[k]) st[k * st_stride] = st_pack(sqrtf(fminf(gfar, lmin)) * (1.0f - 1e-5f), ws[k]);
     }
     lap(2);
 }
@@ -479,6 +481,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     // SCREEN only: fp32 copy of the candidates and per-wave fallback queues
     float2* candf = reinterpret_cast<float2*>(cand + cap);
     float4* box8 = reinterpret_cast<float4*>(candf + cap);   // PRUNE: [cap/8] sub-chunk boxes
+    // PRUNE: per-query state carried across iterations in LDS instead of
+    // registers (fewer VGPRs live through the window scan): last match and
+    // the clearance word, slot k * BLOCK + tid
+    int* qprev = reinterpret_cast<int*>(box8 + cap / kSub);
+    uint32_t* qst = reinterpret_cast<uint32_t*>(qprev + BLOCK * QPT);
 
     // pair of this workgroup: launch order or the scheduler's order
     const int b = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
@@ -545,12 +552,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             box8[c] = make_float4(x0, y0, x1, y1);
         }
     }
-    int bprev[QPT];
-    uint32_t st[QPT];   // PRUNE: clearance state (radius | window start), see st_pack
+    int bprev[QPT];   // !PRUNE screen: last match in registers
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
         bprev[k] = -1;
-        st[k] = 0;
+        if constexpr (PRUNE) {
+            qprev[k * BLOCK + tid] = -1;
+            qst[k * BLOCK + tid] = 0;   // clearance state (radius | window start), see st_pack
+        }
     }
     int nscan_total = 0;
     bool screen = false;
@@ -660,7 +669,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const float dl = (sqrtf(fmaf(ey, ey, ex * ex)) +
                                           1e-6f * (fabsf(fx[k]) + fabsf(fy[k]) + fabsf(ex) + fabsf(ey)) + dsig) *
                                          (1.0f + 1e-5f);
-                        st[k] = st_pack((st_radius(st[k]) - dl) * (1.0f - 1e-5f), st_ws(st[k]));
+                        const uint32_t so = qst[k * BLOCK + tid];
+                        qst[k * BLOCK + tid] = st_pack((st_radius(so) - dl) * (1.0f - 1e-5f), st_ws(so));
                     }
                     M1[k] = INFINITY;
                     M2[k] = INFINITY;
@@ -673,7 +683,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 #pragma unroll
                         for (int k = 0; k < QPT; ++k) {
                             const int i = k * BLOCK + tid;
-                            pred[k] = bprev[k] >= 0 ? bprev[k]
+                            const int bp = qprev[k * BLOCK + tid];
+                            pred[k] = bp >= 0 ? bp
                                                     : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
                             vq[k] = i < n1;
                         }
@@ -681,10 +692,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const int nq = min(QPT, (n1 - 64 * wave + BLOCK - 1) / BLOCK);
                         if (QPT > 1 && nq == QPT - 1)
                             nn_window_pruned<QPT, (QPT > 1 ? QPT - 1 : QPT)>(candf, box8, nsub, fx, fy, vq, pred,
-                                                                               st, M1, M2, C1, nscan_total,
+                                                                               qst + tid, BLOCK, M1, M2, C1,
+                                                                               nscan_total,
                                                                                stamping, tsub, counting, nev);
                         else
-                            nn_window_pruned<QPT, QPT>(candf, box8, nsub, fx, fy, vq, pred, st, M1, M2, C1,
+                            nn_window_pruned<QPT, QPT>(candf, box8, nsub, fx, fy, vq, pred, qst + tid, BLOCK, M1, M2, C1,
                                                        nscan_total, stamping, tsub, counting, nev);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
@@ -777,7 +789,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
             stamp(2);
 #pragma unroll
-            for (int k = 0; k < QPT; ++k) bprev[k] = k * BLOCK + tid < n1 ? bi[k] : -1;
+            for (int k = 0; k < QPT; ++k) {
+                const int nb = k * BLOCK + tid < n1 ? bi[k] : -1;
+                if constexpr (PRUNE) qprev[k * BLOCK + tid] = nb;
+                else bprev[k] = nb;
+            }
         } else {
             // ---- exact fp64 scan (src/icp.py:62-63) ---------------------------
             double best[QPT];
@@ -1068,12 +1084,19 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     a.stamps = g_icp_stamps;
     a.evals = g_icp_evals;
     a.cand_cap = max_n2 < kCandCap ? ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk : kCandCap;
-    const int mode = max_n2 <= kCandCap ? g_screen : 0;
-    size_t lds = red_doubles(inst->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
-    if (mode >= 1)
-        lds += static_cast<size_t>(a.cand_cap) * sizeof(float2);
-    if (mode == 2)
-        lds += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4);
+    int mode = max_n2 <= kCandCap ? g_screen : 0;
+    auto lds_of = [&](int m) {
+        size_t l = red_doubles(inst->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2);
+        if (m >= 1) l += static_cast<size_t>(a.cand_cap) * sizeof(float2);
+        if (m == 2)
+            l += static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
+                 static_cast<size_t>(inst->block) * inst->qpt * 2 * sizeof(int32_t);
+        return l;
+    };
+    // the pruned screen's per-query LDS state does not fit next to 4,096
+    // candidates for the largest query shapes: the full screen (same results) then
+    if (mode == 2 && lds_of(2) > kMaxLds) mode = 1;
+    const size_t lds = lds_of(mode);
     const bool diag = (a.stamps || a.evals) && mode == 2 && !step;   // diagnostics: pruned batch only
     KernelFn fn = mode == 2 ? (step ? inst->step_prune : (diag ? inst->batch_prune_diag : inst->batch_prune))
                 : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)

@@ -398,3 +398,22 @@ def test_understated_bounds_are_flagged(k):
     good = k.IcpBatch(ss, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
     good.launch()
     assert (good.result().iters > 0).all()
+
+
+def test_large_query_scan_lds_fallback(k, oracle):
+    """A 6,000-point query scan against 4,000 candidates: the 512x16 instance's
+    per-query LDS state does not fit beside 4,096 candidates, so the launch
+    takes the full fp32 screen (same results) instead of the pruned one."""
+    from slamhip import se2
+    rng = np.random.default_rng(5)
+    th = np.sort(rng.uniform(-2.3, 2.3, 4000))
+    r = 3 + 0.5 * np.sin(5 * th)
+    pc2 = np.c_[r * np.cos(th), r * np.sin(th)]
+    th1 = np.sort(rng.uniform(-2.3, 2.3, 6000))
+    r1 = 3 + 0.5 * np.sin(5 * th1)
+    T = se2.pose_to_mat([0.05, -0.03, 0.02])
+    pc1 = (np.linalg.inv(T) @ np.c_[r1 * np.cos(th1), r1 * np.sin(th1), np.ones(6000)].T).T[:, :2]
+    res = k.icp_batch([pc1, pc2], [0], [1], np.eye(3)[None], epsilon=0.05, max_iters=30)
+    h, e = oracle.icp(homog(pc1), homog(pc2), np.eye(3), 0.05, 30)
+    assert res.iters[0] == len(h) - 1
+    assert np.abs(res.tf[0] - h[-1]).max() <= TOL

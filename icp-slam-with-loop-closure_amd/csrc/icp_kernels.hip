@@ -615,7 +615,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
 
     unsigned long long tph[5] = {0, 0, 0, 0, 0}, tprev = 0, tsub[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
-    const bool stamping = DIAG && a.stamps != nullptr && b == 0 && wave == 0;   // wave-uniform
+    // diagnostics: workgroup 0; wave 0 writes the sub-phase detail, every wave
+    // its own phase totals (stamps[16 + 8 * wave + ...])
+    const bool stamping = DIAG && a.stamps != nullptr && b == 0;   // wave-uniform
+    int nfail = 0;
     const bool counting = DIAG && a.evals != nullptr;
     unsigned long long nev = 0;
     auto stamp = [&](int ph) {
@@ -627,6 +630,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     };
     auto flush_stamps = [&]() {
         if (stamping && lane == 0) {
+            unsigned long long* ws8 = a.stamps + 16 + 8 * wave;
+            for (int q = 0; q < 4; ++q) ws8[q] = tph[q];
+            ws8[4] = static_cast<unsigned long long>(nscan_total);
+            ws8[5] = static_cast<unsigned long long>(nfail);
+            ws8[6] = tsub[3];
+            ws8[7] = tsub[4];
+        }
+        if (stamping && lane == 0 && wave == 0) {
             for (int q = 0; q < 4; ++q) a.stamps[q] = tph[q];
             a.stamps[4] = static_cast<unsigned long long>(nscan_total);   // sub-chunks visited (wave 0)
             for (int q = 0; q < 9; ++q) a.stamps[5 + q] = tsub[q];
@@ -758,6 +769,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     // this group: the whole wave scans pc2 for it, a (distance, index)
                     // butterfly leaves the first minimum in every lane, the owner takes it
                     uint64_t fails = __ballot(!ok);
+                    if (stamping) nfail += __popcll(fails);
                     if (counting) nev += static_cast<unsigned long long>(n2) * __popcll(fails);
                     while (fails) {
                         const int src = static_cast<int>(__builtin_ctzll(fails));

@@ -207,6 +207,9 @@ int slam_gn_set_stamps(void* dev_buf);
 int slam_gn_set_solver(int mode);
 /* Block rows of the cyclic-reduction solver for (nv, W), 0 = not applicable. */
 int slam_gn_bcr_block_rows(int32_t nv, int32_t W);
+/* Diagnostics: per-phase s_memtime totals of workgroup 0 into a device buffer of
+ * >= 144 uint64 (wave 0's sub-phases in [0, 16), every wave's phase totals in
+ * [16 + 8 * wave, 24 + 8 * wave)); NULL turns stamping off. */
 int slam_icp_set_stamps(void* dev_buf);
 /* Count candidate-distance evaluations performed (all lanes) into a device
  * uint64 (atomic add per wave); NULL turns counting off.  Stamps and the

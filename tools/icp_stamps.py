@@ -17,7 +17,7 @@ ss = k.ScanSet(seq.scans)
 batch = k.IcpBatch(ss, np.arange(1, pairs + 1), np.arange(0, pairs), inits, epsilon=0.05, max_iters=100)
 _abi.lib().slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
 batch.launch()
-buf = torch.zeros(16, dtype=torch.int64, device="cuda")
+buf = torch.zeros(160, dtype=torch.int64, device="cuda")
 _abi.lib().slam_icp_set_stamps(buf.data_ptr())
 batch.launch()
 torch.cuda.synchronize()

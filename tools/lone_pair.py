@@ -46,9 +46,23 @@ for p in pairs:
             ts.append(e0.elapsed_time(e1))
         its = int(batch.result().iters[0])
         line.append(f"{name}:{np.median(ts) * 1e3 / its:.1f}")
+        if "--stamps-all" in sys.argv:   # per-instance phase stamps (wave 0), cycles per iteration
+            sb = torch.zeros(160, dtype=torch.int64, device="cuda")
+            lib.slam_icp_set_stamps(sb.data_ptr())
+            k.IcpBatch(ss, [p + 1], [p], init, epsilon=0.05, max_iters=100).launch()
+            torch.cuda.synchronize()
+            lib.slam_icp_set_stamps(None)
+            t = sb.cpu().numpy().astype(float) / its
+            line[-1] += f"[scan {t[0]:.0f} cert {t[1]:.0f} red {t[3]:.0f} win {t[5]:.0f} clr {t[6]:.0f} vis {t[7]:.0f} b {t[9]:.1f}]"
+            if f"--waves={name}" in sys.argv:   # every wave's totals per iteration
+                nw = int(name.split("x")[0]) // 64
+                w8 = t[16:16 + 8 * nw].reshape(nw, 8)
+                print(f"   {name} per wave: " + " | ".join(
+                    f"w{w}: scan {r[0]:.0f} cert {r[1]:.0f} red {r[3]:.0f} vis {r[4]:.1f} fail {r[5]:.2f} live {r[6]:.1f} b {r[7]:.1f}"
+                    for w, r in enumerate(w8)), flush=True)
     lib.slam_icp_force_instance(-1)
     print(f"pair {p} iters {its} us/iter " + " ".join(line), flush=True)
-    buf = torch.zeros(16, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(160, dtype=torch.int64, device="cuda")
     lib.slam_icp_set_stamps(buf.data_ptr())
     batch2 = k.IcpBatch(ss, [p + 1], [p], init, epsilon=0.05, max_iters=100)
     batch2.launch()

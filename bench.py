@@ -36,8 +36,6 @@ sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
 FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (spec), MI355X_MICROARCH.md
 FP32_VALU_PEAK_TFLOPS = 157.3    # MI355X vector FP32 (spec)
 HBM_PEAK_GBPS = 8000.0
-VALU_SIMDS = 256 * 4              # 256 CUs x 4 SIMDs
-CLOCK_HZ = 2.4e9
 FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add per candidate distance
 
 
@@ -367,16 +365,21 @@ def main():
     hbm_gbps = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     valu_issue = None
+    valu_per_eval = None
     tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             # measured on tj["pairs"] pairs of this workload; scale to this launch
             traffic = round(tj["icp_batch_bytes_per_launch"] * B / tj.get("pairs", B))
+            # VALU busy fraction of the SIMDs over the kernel's dispatches, measured
+            # by counters in the committed profile (tools/gpu_profile.sh busy pass:
+            # 4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)), and
+            # the VALU lane-instructions issued per candidate distance evaluated
+            if "valu_busy_frac" in tj:
+                valu_issue = round(tj["valu_busy_frac"], 4)
             if "valu_insts_per_launch" in tj:
-                # wave64 VALU instruction = 4 cycles of a SIMD (profiles/r01_ubench_valu.txt)
-                cap = VALU_SIMDS * CLOCK_HZ * (kern_ms * 1e-3) / 4.0
-                valu_issue = round(tj["valu_insts_per_launch"] * B / tj.get("pairs", B) / cap, 4)
+                valu_per_eval = tj["valu_insts_per_launch"] * 64.0 / tj.get("pairs", B)
         except Exception:
             traffic = None
     sel = lib.slam_icp_selected_instance(int(n1.max()))
@@ -416,7 +419,12 @@ def main():
             "brute_force_evals_per_launch": evals,
             "pruning_factor": round(evals / max(performed, 1.0), 2),
             "brute_force_equivalent_evals_per_s": round(evals / (kern_ms * 1e-3), 1),
-            "valu_issue_frac": valu_issue,
+            "valu_busy_frac": valu_issue,
+            "valu_busy_source": "profiles/pmc_traffic.json (rocprofv3 SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE, C3 batch)",
+            "valu_lane_insts_per_candidate_eval": (round(valu_per_eval * B / performed, 2)
+                                                   if valu_per_eval and performed else None),
+            "brute_force_equivalent_note": "pruning skips candidates exactly; the brute-force-equivalent rate is "
+                                           "not a roofline figure",
             "hbm": {"achieved": round(hbm_gbps, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 6), "algorithmic_bytes_per_launch": alg_bytes},
         },

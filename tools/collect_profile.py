@@ -39,14 +39,16 @@ def main(tag):
     vals = {}
     rows_out = []
     for names, sub in ((("FETCH_SIZE",), "pmc_fetch"), (("WRITE_SIZE",), "pmc_write"),
-                       (("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"), "pmc_inst")):
+                       (("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"), "pmc_inst"),
+                       (("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
+                         "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE"), "pmc_busy")):
         d = os.path.join(src, sub)
         if not os.path.isdir(d):
             continue
         f = [x for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
         for r in csv.DictReader(open(os.path.join(d, f))):
             if "icp_kernel" in r["Kernel_Name"] and r["Counter_Name"] in names:
-                name = r["Counter_Name"]
+                name = r["Counter_Name"] if sub != "pmc_busy" or r["Counter_Name"] != "SQ_INSTS_VALU" else "busy_SQ_INSTS_VALU"
                 vals[name] = vals.get(name, 0.0) + float(r["Counter_Value"])
                 rows_out.append({k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                                    "VGPR_Count", "SGPR_Count", "Counter_Name", "Counter_Value")})
@@ -66,6 +68,19 @@ def main(tag):
                     "lds_insts_per_launch": vals["SQ_INSTS_LDS"], "waves_per_launch": vals["SQ_WAVES"],
                     "inst_method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES (wave-level "
                                    "instruction counts, summed over the launch)"})
+    if "SQ_ACTIVE_INST_VALU" in vals and "GRBM_GUI_ACTIVE" in vals:
+        simd_cycles = 1024.0 * vals["GRBM_GUI_ACTIVE"] / 8.0     # 256 CUs x 4 SIMDs; GRBM summed over 8 XCDs
+        out.update({
+            "valu_busy_frac": 4.0 * vals["SQ_ACTIVE_INST_VALU"] / simd_cycles,
+            "active_inst_any_frac": 4.0 * vals["SQ_ACTIVE_INST_ANY"] / simd_cycles,
+            "wave_wait_any_over_wave_cycles": vals["SQ_WAIT_ANY"] / max(vals["SQ_WAVE_CYCLES"], 1.0),
+            "wave_wait_inst_any_over_wave_cycles": vals["SQ_WAIT_INST_ANY"] / max(vals["SQ_WAVE_CYCLES"], 1.0),
+            "busy_counters": {k: vals[k] for k in ("SQ_ACTIVE_INST_VALU", "busy_SQ_INSTS_VALU", "SQ_WAVE_CYCLES",
+                                                   "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                   "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE") if k in vals},
+            "busy_method": "rocprofv3 --pmc SQ_ACTIVE_INST_VALU ... GRBM_GUI_ACTIVE (one pass, icp_kernel dispatches "
+                           "summed): valu_busy_frac = 4 x SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) / "
+                           "(1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)"})
     json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -17,4 +17,9 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_wri
     python3 tools/prof_icp.py 10000 1 > $OUT/pmc_write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d $OUT/pmc_inst -o i -- \
     python3 tools/prof_icp.py 10000 1 > $OUT/pmc_inst.log 2>&1
+# VALU busy fraction from counters (not an assumed cycles-per-instruction):
+# SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) x 4 over the SIMD-cycles
+# of the dispatch (GRBM_GUI_ACTIVE, summed over the 8 XCDs)
+timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE \
+    --output-format csv -d $OUT/pmc_busy -o b -- python3 tools/prof_icp.py 10000 1 > $OUT/pmc_busy.log 2>&1
 find $OUT -name "*.csv" | head -20

@@ -278,3 +278,16 @@ def test_pipeline_gn_reduces_drift():
     def ate(p):   # position error after aligning the first pose (the chain starts at odometry[0])
         return float(np.sqrt(np.mean(np.sum((p[:, :2] - s.truth[:, :2]) ** 2, axis=1))))
     assert ate(pg.poses) < 0.7 * ate(r.poses)
+
+
+def test_plan_cache_keys_on_structure():
+    """optimize_pose_graph re-uses the symbolic plan of an identical structure
+    and never the plan of a different one."""
+    from slamhip import gn
+    ea = np.array([0, 1, 2, 0], np.int32)
+    eb = np.array([1, 2, 3, 3], np.int32)
+    p1 = gn.plan_for(4, ea, eb)
+    assert gn.plan_for(4, ea.copy(), eb.copy()) is p1
+    p2 = gn.plan_for(4, ea, np.array([1, 2, 3, 2], np.int32))
+    assert p2 is not p1 and p2.n_slots != p1.n_slots or not np.array_equal(p2.slot_items, p1.slot_items)
+    assert gn.plan_for(5, ea, eb) is not p1

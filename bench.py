@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--instance", type=int, default=-1, help="force a kernel instance (diagnostics)")
     p.add_argument("--sched-probe", type=int, default=-1,
                    help="phase-1 iterations of the batch scheduler (0 = one launch; -1 = library default)")
+    p.add_argument("--sched-heads", type=int, default=-1,
+                   help="pairs started on CU-exclusive workgroups in phase 2 (-1 = library default)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
     return p.parse_args()
 
@@ -285,7 +287,9 @@ def main():
     if args.instance >= 0:
         lib.slam_icp_force_instance(args.instance)
     if args.sched_probe >= 0:
-        lib.slam_icp_set_schedule(args.sched_probe, 2048)
+        lib.slam_icp_set_schedule(args.sched_probe, 1024)
+    if args.sched_heads >= 0:
+        lib.slam_icp_set_schedule_heads(args.sched_heads)
     lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)

@@ -1088,9 +1088,10 @@ static int g_screen = 2;
 static unsigned long long* g_icp_stamps = nullptr;
 static unsigned long long* g_icp_evals = nullptr;
 
+// inst_override / lds_min: the scheduler's CU-exclusive head launch (below)
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
-                  void* stream) {
-    const Instance* inst = pick_instance(max_n1, g_forced_instance);
+                  void* stream, const Instance* inst_override = nullptr, size_t lds_min = 0) {
+    const Instance* inst = inst_override ? inst_override : pick_instance(max_n1, g_forced_instance);
     if (!inst) return fail(SLAM_ETOOBIG, "query scan of %d points exceeds capacity %d", max_n1, kMaxQuery);
     IcpArgs a = args;
     a.stamps = g_icp_stamps;
@@ -1108,7 +1109,7 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     // the pruned screen's per-query LDS state does not fit next to 4,096
     // candidates for the largest query shapes: the full screen (same results) then
     if (mode == 2 && lds_of(2) > kMaxLds) mode = 1;
-    const size_t lds = lds_of(mode);
+    const size_t lds = max(lds_of(mode), lds_min);
     const bool diag = (a.stamps || a.evals) && mode == 2 && !step;   // diagnostics: pruned batch only
     KernelFn fn = mode == 2 ? (step ? inst->step_prune : (diag ? inst->batch_prune_diag : inst->batch_prune))
                 : mode == 1 ? (step ? inst->step_screen : inst->batch_screen)
@@ -1131,8 +1132,48 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
-static int g_sched_probe = 5;          // phase-1 iterations (0: single launch; 4-6 best on C3)
-static int g_sched_min_pairs = 2048;   // batches below this fit the GPU in ~2 waves
+static int g_sched_probe = 4;          // phase-1 iterations (0: single launch; 4-5 best on C3)
+static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
+// Phase 2 starts the pairs the probe keyed slowest (the top g_sched_heads, at
+// most one per 16 pairs) on workgroups that request the whole LDS of a CU, so
+// no other workgroup shares their CU, with an 8-wave instance (a lone pair's
+// iteration latency: 512x3 ~19-21 us vs 256x5 ~29 us on C3's longest pair)
+// beside the rest, which runs on a second stream: the long tail bounds a
+// sharded stream (64 heads measured best: 5,000 / 2,500 /
+// 1,250-pair shards 3.47 / 3.10 / 2.31 -> 2.88 / 2.41 / 1.79 ms, 10k pairs
+// unchanged).  Those pairs' sums run over another wave layout: results equal
+// the single launch to rounding (correspondences exact, iterations equal).
+static int g_sched_heads = 64;
+
+static const Instance* pick_head_instance(int max_n1) {
+    const Instance* best = nullptr;
+    for (int i = 0; i < kNumInstances; ++i) {
+        const Instance& c = kInstances[i];
+        if (c.block != 512 || c.block * c.qpt < max_n1) continue;
+        if (!best || c.qpt < best->qpt) best = &c;
+    }
+    return best;
+}
+
+// per device: the side stream and the fork / join events (created once, reused)
+struct SideStream {
+    hipStream_t stream = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static SideStream* side_stream(int dev) {
+    static SideStream side[64];
+    if (dev < 0 || dev >= 64) return nullptr;
+    SideStream& e = side[dev];
+    if (!e.stream) {
+        if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess) {
+            e.stream = nullptr;
+            return nullptr;
+        }
+    }
+    return &e;
+}
 
 __global__ __launch_bounds__(256) void sched_count_kernel(const int32_t* __restrict__ iters,
                                                           const float* __restrict__ key, int32_t B,
@@ -1197,7 +1238,27 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         a.phase_cap = 0;
         a.resume = 1;
         a.order = order;
-        rc = launch(false, a, B, max_n1, max_n2, stream);
+        const int heads = g_sched_heads > 0 ? min(g_sched_heads, max(B / 16, 1)) : 0;
+        const Instance* hinst = heads > 0 && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
+        int dev = 0;
+        SideStream* side = nullptr;
+        if (hinst && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
+        if (side) {
+            // fork: the head pairs on CU-exclusive workgroups first on the caller's
+            // stream (the GPU is empty after the scheduler kernels: they take the
+            // first CUs), the rest on the side stream behind the fork event, which
+            // resolves after the heads are queued; join before the workspace is freed
+            if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
+                rc = fail(SLAM_EHIP, "icp scheduler: fork");
+            if (rc == 0) rc = launch(false, a, heads, max_n1, max_n2, stream, hinst, kMaxLds);
+            IcpArgs t = a;
+            t.order = order + heads;
+            if (rc == 0) rc = launch(false, t, B - heads, max_n1, max_n2, side->stream);
+            if (rc == 0 && hipEventRecord(side->join, side->stream) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: join");
+            if (rc == 0 && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: wait");
+        } else {
+            rc = launch(false, a, B, max_n1, max_n2, stream);
+        }
     }
     (void)hipFreeAsync(ws, s);
     return rc;
@@ -1239,6 +1300,11 @@ int slam_icp_set_eval_counter(void* dev_u64) {
 // Phased scheduling of large batches (see launch_batch): phase-1 iterations
 // (0 = one launch) and the smallest batch it applies to.  Results do not
 // depend on it (tests/test_icp_gpu.py::test_schedule_is_invisible).
+int slam_icp_set_schedule_heads(int heads) {
+    if (heads < 0) return fail(SLAM_EINVAL, "schedule: negative head count");
+    g_sched_heads = heads;
+    return ok();
+}
 int slam_icp_set_schedule(int probe_iters, int min_pairs) {
     if (probe_iters < 0 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: negative argument");
     g_sched_probe = probe_iters;

@@ -199,8 +199,14 @@ int slam_icp_set_screen(int mode);
  * every pair runs probe_iters iterations, then the unfinished ones resume in
  * order of their last error change (slowest-converging first), so the long
  * tail of iteration counts does not start late.  probe_iters = 0: one launch.
- * Defaults (5, 2048).  Results are identical either way. */
+ * Defaults (4, 1024).  Results are identical either way (with heads = 0). */
 int slam_icp_set_schedule(int probe_iters, int min_pairs);
+/* Phase 2 of the scheduler starts the (at most) `heads` pairs the probe keyed
+ * slowest (one per 128 pairs at most) on CU-exclusive 512-thread workgroups on
+ * a second stream, joined back before the call's work ends: the strong-scaling
+ * tail.  Their sums run over another wave layout, so their results equal the
+ * single launch to rounding (iterations equal).  0 = off; default 16. */
+int slam_icp_set_schedule_heads(int heads);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver: 0 auto (block cyclic reduction when the band allows it),
  * 1 band Cholesky, 2 block cyclic reduction (falls back to 1 if not allowed). */

@@ -322,6 +322,7 @@ def test_schedule_is_invisible(k):
     src, dst = np.arange(1, n + 1), np.arange(0, n)
     outs = []
     try:
+        assert lib.slam_icp_set_schedule_heads(0) == 0   # bit-identity of the phases alone
         for probe in (0, 1, 3, 8, 17):
             assert lib.slam_icp_set_schedule(probe, 1) == 0
             outs.append(k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True))
@@ -330,7 +331,8 @@ def test_schedule_is_invisible(k):
         assert lib.slam_icp_set_schedule(0, 1) == 0
         ref_ro = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=6, rotation_only=True)
     finally:
-        lib.slam_icp_set_schedule(5, 2048)
+        lib.slam_icp_set_schedule(4, 1024)
+        lib.slam_icp_set_schedule_heads(64)
     a = outs[0]
     assert a.iters.min() < 8 < a.iters.max()
     for o in outs[1:-1]:
@@ -344,7 +346,10 @@ def test_schedule_is_invisible(k):
 
 def test_default_schedule_large_batch(k):
     """A batch above the scheduler threshold (2,100 pairs) through the default
-    two-phase path equals the single launch bit for bit."""
+    two-phase path: without head pairs it equals the single launch bit for bit;
+    with the default CU-exclusive head launch (16 slowest-keyed pairs on the
+    512-thread instance, whose sums run in another order) iterations are equal
+    and transforms agree to rounding."""
     from slamhip import _abi
     lib = _abi.lib()
     n = 2100
@@ -352,13 +357,19 @@ def test_default_schedule_large_batch(k):
     src, dst = np.arange(1, n + 1), np.arange(0, n)
     phased = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
     try:
-        assert lib.slam_icp_set_schedule(0, 2048) == 0
+        assert lib.slam_icp_set_schedule_heads(0) == 0
+        plain = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
+        assert lib.slam_icp_set_schedule(0, 1024) == 0
         single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
     finally:
-        lib.slam_icp_set_schedule(5, 2048)
+        lib.slam_icp_set_schedule(4, 1024)
+        lib.slam_icp_set_schedule_heads(64)
     assert phased.iters.max() > 5
+    assert np.array_equal(plain.iters, single.iters)
+    assert np.array_equal(plain.tf, single.tf) and np.array_equal(plain.err, single.err)
     assert np.array_equal(phased.iters, single.iters)
-    assert np.array_equal(phased.tf, single.tf) and np.array_equal(phased.err, single.err)
+    assert np.abs(phased.tf - single.tf).max() <= 1e-12
+    assert np.all(np.abs(phased.err - single.err) <= 1e-12 * np.maximum(1.0, single.err))
 
 
 def test_default_schedule_c3_shape_vs_oracle(k, oracle):

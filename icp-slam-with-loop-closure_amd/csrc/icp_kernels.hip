@@ -1144,6 +1144,8 @@ static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // unchanged).  Those pairs' sums run over another wave layout: results equal
 // the single launch to rounding (correspondences exact, iterations equal).
 static int g_sched_heads = 64;
+// a full C3 batch (10k pairs) keeps every CU for the bulk: heads there cost ~3 %
+constexpr int kHeadsMaxPairs = 8192;
 
 static const Instance* pick_head_instance(int max_n1) {
     const Instance* best = nullptr;
@@ -1238,7 +1240,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         a.phase_cap = 0;
         a.resume = 1;
         a.order = order;
-        const int heads = g_sched_heads > 0 ? min(g_sched_heads, max(B / 16, 1)) : 0;
+        const int heads = g_sched_heads > 0 && B < kHeadsMaxPairs ? min(g_sched_heads, max(B / 16, 1)) : 0;
         const Instance* hinst = heads > 0 && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
         int dev = 0;
         SideStream* side = nullptr;

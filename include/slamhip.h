@@ -202,10 +202,12 @@ int slam_icp_set_screen(int mode);
  * Defaults (4, 1024).  Results are identical either way (with heads = 0). */
 int slam_icp_set_schedule(int probe_iters, int min_pairs);
 /* Phase 2 of the scheduler starts the (at most) `heads` pairs the probe keyed
- * slowest (one per 128 pairs at most) on CU-exclusive 512-thread workgroups on
- * a second stream, joined back before the call's work ends: the strong-scaling
- * tail.  Their sums run over another wave layout, so their results equal the
- * single launch to rounding (iterations equal).  0 = off; default 16. */
+ * slowest (one per 16 pairs at most) first, on CU-exclusive 512-thread
+ * workgroups; the rest runs beside them on a library-owned second stream,
+ * joined back before the call's work ends: the strong-scaling tail.  Batches
+ * below 8,192 pairs only (a full C3 batch keeps every CU for the bulk).  Their
+ * sums run over another wave layout, so their results equal the single launch
+ * to rounding (iterations equal).  0 = off; default 64. */
 int slam_icp_set_schedule_heads(int heads);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver: 0 auto (block cyclic reduction when the band allows it),

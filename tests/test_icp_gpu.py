@@ -428,3 +428,4 @@ def test_large_query_scan_lds_fallback(k, oracle):
     h, e = oracle.icp(homog(pc1), homog(pc2), np.eye(3), 0.05, 30)
     assert res.iters[0] == len(h) - 1
     assert np.abs(res.tf[0] - h[-1]).max() <= TOL
+

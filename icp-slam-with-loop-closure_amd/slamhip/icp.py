@@ -136,6 +136,83 @@ def icp_batch(scans, src, dst, init, epsilon=0.01, max_iters=100, stopping_thres
     return batch.result()
 
 
+class _PairStaging:
+    """Pinned host and device byte buffers reused by single-pair calls: one
+    host->device copy of every input, one device->host copy of every output."""
+
+    def __init__(self, device):
+        self.device = device
+        self.cap_in = self.cap_out = 0
+
+    def buffers(self, n_in, n_out):
+        t = dv.torch()
+        if n_in > self.cap_in:
+            self.cap_in = max(n_in, 2 * self.cap_in)
+            self.h_in = t.empty(self.cap_in, dtype=t.uint8).pin_memory()
+            self.d_in = t.empty(self.cap_in, dtype=t.uint8, device=self.device)
+        if n_out > self.cap_out:
+            self.cap_out = max(n_out, 2 * self.cap_out)
+            self.h_out = t.empty(self.cap_out, dtype=t.uint8).pin_memory()
+            self.d_out = t.empty(self.cap_out, dtype=t.uint8, device=self.device)
+        return self.h_in, self.d_in, self.h_out, self.d_out
+
+
+_STAGING = {}
+
+
+def _a16(n):
+    return (n + 15) // 16 * 16
+
+
+def icp_pair(pc1, pc2, init, epsilon=0.01, max_iters=100, stopping_thresh=0.0001, rotation_only=False):
+    """ONE pair with its transform history (the drop-in ``icp()``'s call):
+    inputs packed into one pinned staging buffer (one copy in), outputs in one
+    device buffer (one copy out).  Returns (hist (iters+1, 3, 3), err, iters)."""
+    t = dv.require_gpu()
+    a, b = _xy(pc1), _xy(pc2)
+    n1, n2 = len(a), len(b)
+    if n1 > _abi.lib().slam_icp_max_query_points():
+        raise ValueError(f"pc1 of {n1} points exceeds the kernel capacity {_abi.lib().slam_icp_max_query_points()}")
+    T0 = _se2_rows(init, 1)
+    max_iters = int(max_iters)
+    stride = max_iters + 3
+    o_pts, o_off = 0, _a16(16 * (n1 + n2))
+    o_idx, o_init = o_off + 32, o_off + 48
+    n_in = o_init + 80
+    o_hist, o_tf = 0, _a16(72 * stride)
+    o_err, o_it = o_tf + 80, o_tf + 96
+    n_out = o_it + 16
+    dev = t.cuda.current_device()
+    st = _STAGING.get(dev)
+    if st is None:
+        st = _STAGING[dev] = _PairStaging(t.device("cuda", dev))
+    h_in, d_in, h_out, d_out = st.buffers(n_in, n_out)
+    stream = t.cuda.current_stream()
+    stream.synchronize()   # the staging buffers of the previous call are free
+    hb = h_in.numpy()
+    pts = np.frombuffer(hb, dtype=np.float64, count=2 * (n1 + n2), offset=o_pts).reshape(-1, 2)
+    pts[:n1] = a
+    pts[n1:] = b
+    np.frombuffer(hb, dtype=np.int64, count=3, offset=o_off)[:] = (0, n1, n1 + n2)
+    np.frombuffer(hb, dtype=np.int32, count=2, offset=o_idx)[:] = (0, 1)
+    np.frombuffer(hb, dtype=np.float64, count=9, offset=o_init)[:] = T0[0]
+    d_in[:n_in].copy_(h_in[:n_in], non_blocking=True)
+    base, ob = d_in.data_ptr(), d_out.data_ptr()
+    _abi.check(_abi.lib().slam_icp_batch_f64(
+        base + o_pts, base + o_off, base + o_idx, base + o_idx + 4, base + o_init, 1, float(epsilon), max_iters,
+        float(stopping_thresh), int(bool(rotation_only)), n1, n2, stride, ob + o_hist, ob + o_tf, ob + o_err,
+        ob + o_it, stream.cuda_stream), "slam_icp_batch_f64")
+    h_out[:n_out].copy_(d_out[:n_out], non_blocking=True)
+    stream.synchronize()
+    ho = h_out.numpy()
+    iters = int(np.frombuffer(ho, dtype=np.int32, count=1, offset=o_it)[0])
+    if iters == np.iinfo(np.int32).min:   # the kernel flagged the pair: report (and clear) it
+        _abi.check(_abi.lib().slam_icp_status(stream.cuda_stream), "slam_icp_batch_f64")
+    hist = np.frombuffer(ho, dtype=np.float64, count=9 * stride, offset=o_hist).reshape(stride, 3, 3)
+    err = np.float64(np.frombuffer(ho, dtype=np.float64, count=1, offset=o_err)[0])
+    return hist[:iters + 1].copy(), err, iters
+
+
 def icp_pairs(pc1_list, pc2_list, inits, **kw):
     """ICP over explicit (pc1, pc2, init) triples (the shape of the reference's
     ``delayed(icp.icp)(pc1, pc2, init_transform=...)`` fan-out)."""

@@ -64,12 +64,12 @@ def icp(pc1, pc2, init_transform=_DEFAULT_INIT, epsilon=0.01, max_iters=100, sto
     translation zeroed in place when ``rotation_only``, as the reference does).
     """
     init = np.asarray(init_transform, dtype=np.float64)
-    res = _k.icp_batch([pc1, pc2], [0], [1], init[None], epsilon=epsilon, max_iters=max_iters,
-                       stopping_thresh=stopping_thresh, rotation_only=rotation_only, history=True)
+    hist, err, _ = _k.icp_pair(pc1, pc2, init, epsilon=epsilon, max_iters=max_iters,
+                               stopping_thresh=stopping_thresh, rotation_only=rotation_only)
     if rotation_only:
         init_transform[:2, 2] = 0
-    transforms = [init_transform] + [h.copy() for h in res.hist[0][1:]]
-    return transforms, np.float64(res.err[0])
+    transforms = [init_transform] + [h.copy() for h in hist[1:]]
+    return transforms, np.float64(err)
 
 
 def icp_batch(pc1_list, pc2_list, init_transforms, epsilon=0.01, max_iters=100, stopping_thresh=0.0001,

@@ -23,7 +23,10 @@
  *     stream-ordered workspace (hipMallocAsync / hipFreeAsync, 12 B per pair),
  *     which stream capture records as graph memory nodes;
  *   - return 0 on success, a negative SLAM_E* code on failure; the message is
- *     available from slam_last_error() (thread-local).
+ *     available from slam_last_error() (thread-local);
+ *   - one host thread per device at a time: the diagnostics switches are
+ *     process-global and the batch scheduler's second stream and fork / join
+ *     events are one set per device.
  */
 #ifndef SLAMHIP_H
 #define SLAMHIP_H

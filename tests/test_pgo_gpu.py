@@ -2,8 +2,9 @@
 recompute) against the reference's golden outputs and the CPU oracle.
 
 Tolerance: positions within 1e-9 after 20 SGD steps of the reference's lap
-graph; headings compared modulo 2 pi (the reference lets theta drift by
-multiples of 2 pi).
+graph; headings both modulo 2 pi and as the drifting values themselves (the
+reference lets theta drift by multiples of 2 pi) to 1e-9
+relative; the C4-size and global-memory-path graphs to the same bounds.
 """
 import numpy as np
 import pytest
@@ -38,6 +39,8 @@ def test_sgd_golden_steps(golden):
             ref = s[f"poses_step{k + 1}"]
             assert np.abs(pg.poses[:, :2] - ref[:, :2]).max() <= TOL, k
             assert np.abs(_wrap(pg.poses[:, 2] - ref[:, 2])).max() <= TOL, k
+            # not only modulo 2 pi: the drifting headings themselves, to 1e-9 relative
+            assert np.all(np.abs(pg.poses[:, 2] - ref[:, 2]) <= TOL * np.maximum(1.0, np.abs(ref[:, 2]))), k
     assert pg.poses is poses_obj     # updated in place
     pgo.recompute_pose_graph_orientation(pg, None, 100, 0.05, 1, icp_recompute=False)
     assert np.abs(pg.poses - s["poses_recomputed"]).max() <= TOL
@@ -81,8 +84,9 @@ def test_sgd_large_graph_vs_oracle():
     ref = poses.copy()
     po.sgd_step(ref, ea, eb, tf, learning_rate=1.0)
     got = pgo.sgd_step(poses, ea, eb, tf, learning_rate=1.0)
-    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-7
-    assert np.abs(_wrap(got[:, 2] - ref[:, 2])).max() <= 1e-7
+    # measured: positions 1e-12, headings 3e-10 on |theta| up to 2e4 (tools/sgd_diff.py)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= TOL
+    assert np.all(np.abs(got[:, 2] - ref[:, 2]) <= TOL * np.maximum(1.0, np.abs(ref[:, 2])))
 
 
 @pytest.mark.parametrize("pps,laps,ncons", [(150, 15, 3000), (875, 40, 250)])
@@ -105,5 +109,5 @@ def test_sgd_global_memory_path_vs_oracle(pps, laps, ncons):
         po.sgd_step(ref, ea, eb, tf, learning_rate=1.0 / (k + 1))
         s.step(1.0 / (k + 1))
     got = s.host_poses()
-    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-7
-    assert np.abs(got[:, 2] - ref[:, 2]).max() <= 1e-9 * max(1.0, np.abs(ref[:, 2]).max())
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= TOL
+    assert np.all(np.abs(got[:, 2] - ref[:, 2]) <= TOL * np.maximum(1.0, np.abs(ref[:, 2])))

@@ -48,32 +48,45 @@ class GnPlan:
         both = (ca >= 0) & (cb >= 0)
         self.W = int(max(2, (np.abs(ca[both] - cb[both]).max() + 2) if both.any() else 2))
 
-        # diagonal slots: free node n, items 2e + side
-        diag_items = [[] for _ in range(N)]
-        pair_items = {}
-        for e in range(len(ea)):
-            a, b = int(ea[e]), int(eb[e])
-            if a == b:
-                continue   # a self-loop has zero Jacobian sum: no H contribution
-            if node_col[a] >= 0:
-                diag_items[a].append(2 * e)
-            if node_col[b] >= 0:
-                diag_items[b].append(2 * e + 1)
-            if node_col[a] >= 0 and node_col[b] >= 0:
-                row, col = (a, b) if node_col[a] > node_col[b] else (b, a)
-                pair_items.setdefault((row, col), []).append(2 * e + (0 if row == a else 1))
-        rc, ptr, items = [], [0], []
-        for n in order:
-            rc.append((node_col[n], node_col[n]))
-            items.extend(diag_items[n])
-            ptr.append(len(items))
-        for (row, col), its in pair_items.items():
-            rc.append((node_col[row], node_col[col]))
-            items.extend(its)
-            ptr.append(len(items))
+        # diagonal slots: free node n (in RCM order), items 2e + side (a: 0, b: 1) in
+        # edge order; pair slots: one per connected free pair (row = the node with
+        # the larger column), in order of first appearance, items in edge order.
+        # Vectorised; the slot and item order is the one the assembly sums in
+        # (tests/test_gn.py::test_plan_matches_loop_construction).
+        e = np.arange(len(ea), dtype=np.int64)
+        ok = ea != eb                                   # a self-loop adds nothing to H
+        rank = np.full(N, -1, dtype=np.int64)
+        rank[order] = np.arange(len(order))
+        fa, fb = ok & (node_col[ea] >= 0), ok & (node_col[eb] >= 0)
+        dn = np.r_[ea[fa], eb[fb]]
+        di = np.r_[2 * e[fa], 2 * e[fb] + 1]
+        de = np.r_[e[fa], e[fb]]
+        srt = np.lexsort((de, rank[dn]))
+        diag_counts = np.bincount(rank[dn], minlength=len(order))
+        both = fa & fb
+        pa, pb, pe = ea[both], eb[both], e[both]
+        a_row = node_col[pa] > node_col[pb]
+        row = np.where(a_row, pa, pb)
+        col = np.where(a_row, pb, pa)
+        key = row.astype(np.int64) * N + col
+        uk, first, inv = np.unique(key, return_index=True, return_inverse=True)
+        prank = np.empty(len(uk), dtype=np.int64)
+        prank[np.argsort(first, kind="stable")] = np.arange(len(uk))
+        pr = prank[inv]
+        psrt = np.lexsort((pe, pr))
+        pitems = 2 * pe + np.where(a_row, 0, 1)
+        prow = np.empty(len(uk), dtype=np.int64)
+        pcol = np.empty(len(uk), dtype=np.int64)
+        prow[pr] = row
+        pcol[pr] = col
+        rc = np.r_[np.stack([node_col[order], node_col[order]], 1).reshape(-1, 2),
+                   np.stack([node_col[prow], node_col[pcol]], 1).reshape(-1, 2)]
+        counts = np.r_[diag_counts, np.bincount(pr, minlength=len(uk))]
+        items = np.r_[di[srt], pitems[psrt]]
+        ptr = np.r_[0, np.cumsum(counts)]
         self.slot_rc = np.asarray(rc, dtype=np.int32).reshape(-1, 2)
         self.slot_ptr = np.asarray(ptr, dtype=np.int32)
-        self.slot_items = np.asarray(items if items else [0], dtype=np.int32)
+        self.slot_items = np.asarray(items if len(items) else [0], dtype=np.int32)
         self.n_slots = len(rc)
 
 

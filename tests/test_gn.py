@@ -291,3 +291,55 @@ def test_plan_cache_keys_on_structure():
     p2 = gn.plan_for(4, ea, np.array([1, 2, 3, 2], np.int32))
     assert p2 is not p1 and p2.n_slots != p1.n_slots or not np.array_equal(p2.slot_items, p1.slot_items)
     assert gn.plan_for(5, ea, eb) is not p1
+
+
+def _loop_plan_slots(N, ea, eb, node_col, order):
+    """The per-edge loop construction of the H slot lists (the plan's original
+    form), kept as the reference for the vectorised one."""
+    diag_items = [[] for _ in range(N)]
+    pair_items = {}
+    for e in range(len(ea)):
+        a, b = int(ea[e]), int(eb[e])
+        if a == b:
+            continue
+        if node_col[a] >= 0:
+            diag_items[a].append(2 * e)
+        if node_col[b] >= 0:
+            diag_items[b].append(2 * e + 1)
+        if node_col[a] >= 0 and node_col[b] >= 0:
+            row, col = (a, b) if node_col[a] > node_col[b] else (b, a)
+            pair_items.setdefault((row, col), []).append(2 * e + (0 if row == a else 1))
+    rc, ptr, items = [], [0], []
+    for n in order:
+        rc.append((node_col[n], node_col[n]))
+        items.extend(diag_items[n])
+        ptr.append(len(items))
+    for (row, col), its in pair_items.items():
+        rc.append((node_col[row], node_col[col]))
+        items.extend(its)
+        ptr.append(len(items))
+    return np.asarray(rc).reshape(-1, 2), np.asarray(ptr), np.asarray(items if items else [0])
+
+
+@pytest.mark.parametrize("case", ["c4", "random", "selfloops"])
+def test_plan_matches_loop_construction(case):
+    """The vectorised symbolic plan lists the same slots and the same items in
+    the same order as the per-edge loop (the assembly's summation order)."""
+    from slamhip import gn, synthetic
+    rng = np.random.default_rng(3)
+    if case == "c4":
+        guess, ea, eb, _, _ = synthetic.lap_graph_c4()
+        N, fixed = len(guess), 0
+    else:
+        N = 300
+        ea = np.r_[np.arange(N - 1), rng.integers(0, N, 500)]
+        eb = np.r_[np.arange(1, N), rng.integers(0, N, 500)]
+        if case == "selfloops":
+            ea[::37] = eb[::37]          # self-loops, and repeated pairs below
+            ea = np.r_[ea, ea[:40]]
+            eb = np.r_[eb, eb[:40]]
+        fixed = 7
+    p = gn.GnPlan(N, ea, eb, fixed)
+    order = np.argsort(np.where(p.node_col >= 0, p.node_col, np.iinfo(np.int32).max), kind="stable")[:p.nv // 3]
+    rc, ptr, items = _loop_plan_slots(N, np.asarray(ea), np.asarray(eb), p.node_col, order)
+    assert np.array_equal(p.slot_rc, rc) and np.array_equal(p.slot_ptr, ptr) and np.array_equal(p.slot_items, items)

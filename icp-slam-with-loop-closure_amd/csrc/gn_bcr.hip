@@ -33,6 +33,7 @@ constexpr int kBcrThreads = 256;
 #endif
 constexpr int kBcrMaxWb = 96;
 
+
 __host__ __device__ inline int64_t bcr_blk(int Wb) { return static_cast<int64_t>(Wb) * Wb; }
 
 // e -> (e / Wb, e % Wb) for e < Wb^2 <= 96^2 without an integer division: the
@@ -150,18 +151,20 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
                                                                   int32_t Wb, int32_t nb, int32_t s,
                                                                   int32_t* __restrict__ status,
                                                                   unsigned long long* __restrict__ stamps) {
-    // four workgroups per odd block (blockIdx.y = q): each eliminates D_i and carries
-    // NW of the 2T + 1 right-hand-side column tiles — q 0, 1: tiles [0, NW), [NW, T) of
-    // E_p (-> X_i); q 2, 3: tiles [0, NW), [NW, T + 1) of [E_i^T | b_i] (-> Y_i, z_i).
-    // Fewer tiles per workgroup = less work per pivot on the dependent chain.
+    // six workgroups per odd block (blockIdx.y = q): each eliminates D_i and carries
+    // NW of the right-hand-side column tiles — q 0, 1: tiles [0, NW), [NW, T) of
+    // E_p (-> X_i); q 2, 3: tiles [0, NW), [NW, T + 1) of [E_i^T | b_i] (-> Y_i, z_i);
+    // q 4, 5: tiles [0, NW), [NW, T) of the identity (-> C_i^-1, for the back
+    // kernel).  Fewer tiles per workgroup = less work per pivot on the dependent chain.
     constexpr int NW = (T + 2) / 2;
     __shared__ double colb[2][16 * T];
     __shared__ double rowb[2][16 * NW];
     const int q = blockIdx.y;
-    const bool ys = q >= 2;                    // Y side (E_i^T | b_i)
+    const bool iv = q >= 4;                    // C_i^-1: the identity as right-hand side (-> Cs)
+    const bool ys = q == 2 || q == 3;          // Y side (E_i^T | b_i)
     const int w0 = (q & 1) ? NW : 0;           // first global column tile
     const int wend = (q & 1) ? (ys ? T + 1 : T) : NW;
-    const bool owner = q == 2;                 // writes C_i and the status
+    const bool owner = q == 2;                 // writes the status
     const bool stamping = stamps && blockIdx.x == 0 && owner && threadIdx.x == 0;
     unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
     auto lap = [&](int qq) {
@@ -189,7 +192,8 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
             const int w = w0 + wl, C = tc + 16 * w;
             double x = 0.0;
             if (w < wend) {
-                if (!ys) x = Ep[R * Wb + C];
+                if (iv) x = R == C ? 1.0 : 0.0;
+                else if (!ys) x = Ep[R * Wb + C];
                 else if (w < T) x = n < nb ? Ei[C * Wb + R] : 0.0;
                 else x = tc == 0 ? bz[static_cast<int64_t>(i) * Wb + R] : 0.0;
             }
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
     bcr_reg_elim<T, NW>(a, r, colb, rowb, tr, tc, bad, nullptr);
     lap(1);
     if (bad && owner && tid == 0) *status = 1;
-    double* Out = (ys ? Ys : Xs) + i * B2;
+    double* Out = (iv ? Cs : ys ? Ys : Xs) + i * B2;
 #pragma unroll
     for (int u = 0; u < T; ++u) {
         const int R = tr + 16 * u;
@@ -210,13 +214,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_odd_reg_kernel(const double* 
             const int w = w0 + wl;
             if (w < wend && w < T) Out[R * Wb + tc + 16 * w] = r[u][wl];
             if (w < wend && w == T && tc == 0) bz[static_cast<int64_t>(i) * Wb + R] = r[u][wl];
-        }
-        if (owner) {
-#pragma unroll
-            for (int v = 0; v < T; ++v) {
-                const int C = tc + 16 * v;
-                Cs[i * B2 + R * Wb + C] = C <= R ? a[u][v] : 0.0;
-            }
         }
     }
     lap(3);
@@ -447,7 +444,10 @@ __device__ __forceinline__ double dpp_row(double v) {
 
 // Back-substitution of the odd blocks of level s: v = z - X x_p - Y x_n
 // (x_p / x_n staged in LDS, X / Y read in 128 B row segments, DPP row sums),
-// then C^-T v by one wave.
+// then x_i = C_i^-T v as the mat-vec (C_i^-1)^T v over the whole workgroup:
+// the odd kernel's two extra workgroups eliminated [D_i | I] into C_i^-1, so
+// no 80-step triangular solve sits on this level's dependent chain (C4:
+// 10.5 -> ~3 us per level, 1,560 -> 1,623 it/s).
 template <int T>   // T = Wb / 16
 __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __restrict__ Cs,
                                                                const double* __restrict__ Xs,
@@ -459,7 +459,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
     double* Cm = lds;
     double* vv = lds + static_cast<int64_t>(Wb) * ldc;     // [Wb]
     double* xpn = vv + Wb;                                  // [2][Wb]
-    double* rdg = xpn + 2 * Wb;                             // [Wb]
     const int tid = threadIdx.x;
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
@@ -477,7 +476,6 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
         }
     }
     for (int k = tid; k < Wb; k += kBcrThreads) {
-        rdg[k] = 1.0 / Ci[static_cast<int64_t>(k) * Wb + k];
         xpn[k] = x[static_cast<int64_t>(p) * Wb + k];
         xpn[Wb + k] = n < nb ? x[static_cast<int64_t>(n) * Wb + k] : 0.0;
     }
@@ -515,12 +513,34 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
         }
     }
     __syncthreads();
-    if (tid < 64) {
-        double v0 = tid < Wb ? vv[tid] : 0.0, v1 = tid + 64 < Wb ? vv[tid + 64] : 0.0;
-        bcr_backsub_wave(Cm, ldc, rdg, Wb, v0, v1);
-        double* xi = x + static_cast<int64_t>(i) * Wb;
-        if (tid < Wb) xi[tid] = v0;
-        if (tid + 64 < Wb) xi[tid + 64] = v1;
+    {
+        // x_i = (C_i^-1)^T v: thread (c16 = tid >> 4, r16 = tid & 15) sums rows
+        // r16 + 16 u of columns c16 + 16 w; the 16 lanes of a DPP row add up
+        const int r16 = tid & 15, c16 = tid >> 4;
+        double a[T];
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            const int c = c16 + 16 * w;
+            double acc = 0.0;
+#pragma unroll
+            for (int u = 0; u < T; ++u) {
+                const int r = r16 + 16 * u;
+                acc = fma(Cm[r * ldc + c], vv[r], acc);
+            }
+            a[w] = acc;
+        }
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            a[w] += dpp_row<0xB1>(a[w]);
+            a[w] += dpp_row<0x4E>(a[w]);
+            a[w] += dpp_row<0x124>(a[w]);
+            a[w] += dpp_row<0x128>(a[w]);
+        }
+        if (r16 == 0) {
+            double* xi = x + static_cast<int64_t>(i) * Wb;
+#pragma unroll
+            for (int w = 0; w < T; ++w) xi[c16 + 16 * w] = a[w];
+        }
     }
 }
 
@@ -594,7 +614,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     for (; s < nb; s *= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
-        hipLaunchKernelGGL(odd, dim3(n_odd, 4), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
+        hipLaunchKernelGGL(odd, dim3(n_odd, 6), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
                            stamps);
         hipLaunchKernelGGL(even, dim3(n_even, 5), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
     }

@@ -142,4 +142,112 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Order-free sums.  A term x with |x| <= B (one of n terms) is split onto two
+// fixed grids chosen from (B, n) alone: h1 = (x + M1) - M1 is x rounded to a
+// multiple of u1 = ulp(M1) (exact: x + M1 stays inside M1's binade), the
+// remainder r = x - h1 is exact, and h2 = (r + M2) - M2 rounds r to u2 =
+// ulp(M2).  Every partial sum of h1 values (multiples of u1, bounded by
+// 2^53 u1) and of h2 values is exact, so the two totals are the same bits for
+// ANY summation order: any workgroup shape, query layout or split of a pair
+// over workgroups.  The dropped remainder is <= u2 / 2 per term, ~2^-70 of n B
+// (far below a naive fp64 sum's rounding).  Valid while n B < 2^900.
+// ---------------------------------------------------------------------------
+struct RsumGrid {
+    double m1, m2;
+};
+
+__device__ __forceinline__ RsumGrid rsum_grid(double bound, int n) {
+    int e;
+    (void)frexp(fmin(fmax(bound, 0x1p-900), 0x1p+900) * static_cast<double>(n), &e);   // n B < 2^e
+    e += 2;                                                                           // |x| <= 2^(e-2) / n
+    const int lg = 32 - __clz(max(n - 1, 1));                                         // n <= 2^lg
+    RsumGrid g;
+    g.m1 = ldexp(1.5, e);
+    g.m2 = ldexp(1.5, e - 53 + lg + 2);   // |r| <= 2^(e-53) <= 2^(e2-2) / n
+    return g;
+}
+
+__device__ __forceinline__ void rsum_add(double x, const RsumGrid& g, double& s1, double& s2) {
+    const double h1 = (x + g.m1) - g.m1;
+    const double r = x - h1;
+    const double h2 = (r + g.m2) - g.m2;
+    s1 += h1;
+    s2 += h2;
+}
+
+// v_permlane{16,32}_swap on doubles (both 32-bit halves): for a pair (a, b)
+// a + b afterwards is a's sum over the two swapped lane sets in one half (rows)
+// and b's in the other.
+__device__ __forceinline__ void swap32_d(double& a, double& b) {
+    const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(x), static_cast<unsigned>(y), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(x >> 32), static_cast<unsigned>(y >> 32),
+                                                     false, false);
+    a = __longlong_as_double((static_cast<long long>(hi[0]) << 32) | lo[0]);
+    b = __longlong_as_double((static_cast<long long>(hi[1]) << 32) | lo[1]);
+}
+__device__ __forceinline__ void swap16_d(double& a, double& b) {
+    const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(x), static_cast<unsigned>(y), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<unsigned>(x >> 32), static_cast<unsigned>(y >> 32),
+                                                     false, false);
+    a = __longlong_as_double((static_cast<long long>(hi[0]) << 32) | lo[0]);
+    b = __longlong_as_double((static_cast<long long>(hi[1]) << 32) | lo[1]);
+}
+
+// Sum over the 16 lanes of each row; every lane of the row gets it.
+__device__ __forceinline__ double row_sum_d(double v) {
+#define SLAM_DPP_D(v, ctrl)                                                                            \
+    __longlong_as_double(                                                                              \
+        (static_cast<long long>(__builtin_amdgcn_update_dpp(                                           \
+             0, static_cast<int>(__double_as_longlong(v) >> 32), ctrl, 0xF, 0xF, false))                \
+         << 32) |                                                                                      \
+        static_cast<unsigned int>(__builtin_amdgcn_update_dpp(                                         \
+            0, static_cast<int>(__double_as_longlong(v) & 0xffffffff), ctrl, 0xF, 0xF, false)))
+    v += SLAM_DPP_D(v, 0xB1);    // xor 1
+    v += SLAM_DPP_D(v, 0x4E);    // xor 2
+    v += SLAM_DPP_D(v, 0x12C);   // row_ror 12
+    v += SLAM_DPP_D(v, 0x128);   // row_ror 8
+#undef SLAM_DPP_D
+    return v;
+}
+
+// Block all-reduce of 16 per-thread values whose partial sums are all EXACT
+// (rsum_add grids), so the reduction order is free and chosen for cost: a
+// reduce-scatter over the wave halves and row pairs (permlane swaps: 16 -> 8
+// -> 4 values per lane), row sums of the remaining 4, one LDS slot per value
+// and wave, and lane q (< 16) of every wave sums value q over the waves.
+// `slab` is LDS of WAVES * 16 doubles; one barrier.  Returns value q in lane
+// q (readlane_d(ret, q) makes it uniform).
+template <int WAVES>
+__device__ __forceinline__ double block_sum_exact16(double (&v)[16], double* slab) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // lanes 0-31: v[2j] summed over l, l+32; lanes 32-63: v[2j+1]
+        swap32_d(v[2 * j], v[2 * j + 1]);
+        v[j] = v[2 * j] + v[2 * j + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // row r holds v[4i + {0, 2, 1, 3}[r]] summed over l, l+16, l+32, l+48
+        swap16_d(v[2 * i], v[2 * i + 1]);
+        v[i] = v[2 * i] + v[2 * i + 1];
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int row = lane >> 4;
+    const int q0 = ((row & 1) << 1) | (row >> 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double s = row_sum_d(v[i]);
+        if ((lane & 15) == 0) slab[wave * 16 + 4 * i + q0] = s;
+    }
+    __syncthreads();
+    double t = 0.0;
+    if (lane < 16) {
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += slab[w * 16 + lane];
+    }
+    return t;
+}
+
 }  // namespace slamhip

@@ -38,9 +38,13 @@ namespace slamhip {
 constexpr int kCandCap = 4096;
 constexpr size_t kMaxLds = 160 * 1024;      // LDS per workgroup (gfx950)
 constexpr int32_t kBadBounds = INT32_MIN;   // out_iters of a pair outside the launch's bounds
-__device__ int g_icp_status;                // nonzero: some pair was outside its launch's bounds          // pc2 points resident in LDS (64 KiB fp64 + 32 KiB fp32)
-// two reduction slabs of 8 doubles per wave at the front of the dynamic LDS
-__host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 8; }
+__device__ int g_icp_status;                // nonzero: some pair was outside its launch's bounds
+// two reduction slabs of 16 doubles per wave at the front of the dynamic LDS
+// (block_sum_exact16, alternating between iterations), then 16 doubles of
+// per-pair constants (kept in LDS, not in registers across the NN search)
+constexpr int kPairConsts = 16;
+__host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 16 + kPairConsts; }
+enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax };
 
 struct IcpArgs {
     const double2* pts;
@@ -475,7 +479,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* red0 = reinterpret_cast<double*>(smem);
-    double* red1 = red0 + WAVES * 8;
+    double* red1 = red0 + WAVES * 16;
+    double* pconst = red0 + 2 * WAVES * 16;   // PairConst slots
     double2* cand = reinterpret_cast<double2*>(smem + red_doubles(BLOCK) * sizeof(double));
     const int cap = a.cand_cap;
     // SCREEN only: fp32 copy of the candidates and per-wave fallback queues
@@ -521,20 +526,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         return;   // uniform
     }
 
-    double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound)
+    double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound, sum grids)
     if (resident) {
 #pragma unroll kStageUnroll
         for (int j = tid; j < n2; j += BLOCK) {   // unrolled: several loads in flight per thread
             const double2 p = p2[j];
             cand[j] = p;
-            if constexpr (SCREEN) {
-                cf_put(candf, j, static_cast<float>(p.x), static_cast<float>(p.y));
-                cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
-            }
+            if constexpr (SCREEN) cf_put(candf, j, static_cast<float>(p.x), static_cast<float>(p.y));
+            cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
         }
         if constexpr (SCREEN) {
             for (int j = n2 + tid; j < (n2 + kChunk - 1) / kChunk * kChunk; j += BLOCK)
                 cf_put(candf, j, kSentinel, kSentinel);
+        }
+    } else {
+        for (int j = tid; j < n2; j += BLOCK) {
+            const double2 p = p2[j];
+            cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
         }
     }
     const int nsub = (n2 + kChunk - 1) / kChunk * (kChunk / kSub);   // sub-chunks incl. padding
@@ -563,17 +571,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     }
     int nscan_total = 0;
     bool screen = false;
-    float pmax = 0.0f;   // PRUNE: max |coordinate| of pc1 (motion bound slack)
-    if constexpr (SCREEN) {
+    double pmaxd;        // max |coordinate| of pc1 (sum grids)
+    float pmax = 0.0f;   // PRUNE: the same in fp32 (motion bound slack)
+    {
         double cm[2] = {cmax, 0.0};
-        if constexpr (PRUNE) {
 #pragma unroll kStageUnroll
-            for (int i = tid; i < n1; i += BLOCK) {
-                const double2 p = p1[i];
-                cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));
-            }
+        for (int i = tid; i < n1; i += BLOCK) {
+            const double2 p = p1[i];
+            cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));
         }
-        // block max through the sum slab: max is exact, order-free
+        // block max through the second slab: max is exact, order-free
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             cm[0] = fmax(cm[0], __shfl_xor(cm[0], off, 64));
@@ -592,8 +599,45 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             pm = fmax(pm, red1[WAVES + w]);
         }
         cmax = uniform_d(cmax);
+        pmaxd = uniform_d(pm);
         pmax = uniform_f(static_cast<float>(pm) * (1.0f + 1e-6f));
-        screen = cmax < 1e18;   // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
+        // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
+        if constexpr (SCREEN) screen = cmax < 1e18;
+    }
+    // Cross-covariance centre: pc1's first point c (any per-pair constant
+    // works; it only keeps the terms small) and dp = sum(p - c), once per pair
+    // as an order-free sum (first slab; iteration 0 reduces into the second).
+    const double2 pc = p1[0];
+    double dpx, dpy;
+    {
+        const RsumGrid gp = rsum_grid(2.0 * pmaxd * (1.0 + 1e-12), n1);
+        double acc[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+        for (int i = tid; i < n1; i += BLOCK) {
+            const double2 p = p1[i];
+            rsum_add(p.x - pc.x, gp, acc[0], acc[1]);
+            rsum_add(p.y - pc.y, gp, acc[2], acc[3]);
+        }
+        const double t = block_sum_exact16<WAVES>(acc, red0);
+        dpx = readlane_d(t, 0) + readlane_d(t, 1);
+        dpy = readlane_d(t, 2) + readlane_d(t, 3);
+    }
+    if (tid == 0) {   // read back after the barrier before the loop
+        pconst[kPcX] = pc.x;
+        pconst[kPcY] = pc.y;
+        pconst[kDpX] = dpx;
+        pconst[kDpY] = dpy;
+        pconst[kMupX] = pc.x + dpx / static_cast<double>(n1);   // pc1's centroid: mu_p = c + dp / n
+        pconst[kMupY] = pc.y + dpy / static_cast<double>(n1);
+        const RsumGrid gm = rsum_grid(cmax, n1);                         // matched pc2 coordinates
+        const RsumGrid gs = rsum_grid(2.0 * pmaxd * cmax * (1.0 + 1e-12), n1);   // (p - c) m^T terms
+        pconst[kGm1] = gm.m1;
+        pconst[kGm2] = gm.m2;
+        pconst[kGs1] = gs.m1;
+        pconst[kGs2] = gs.m2;
+        pconst[kPmax] = pmaxd;
+        pconst[kCmax] = cmax;
     }
     // PRUNE: this iteration's motion T - T_prev in fp32 and its rounding slack
     float dT[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dsig = 0.0f;
@@ -844,45 +888,70 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             }
         }
 
-        // ---- src/icp.py:64,68  centroids + error ------------------------------
-        double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        double2 mk[QPT];   // matched points of every group at once (one memory latency)
+        // ---- src/icp.py:64,68 + 22-46  error, centroids, cross-covariance ------
+        // One pass, one barrier, order-free sums (rsum_add): the totals are the
+        // same bits for every workgroup shape and query layout, so a pair's
+        // result does not depend on the instance, the scheduler or the number of
+        // GPUs a stream is sharded over.  Per query:
+        //   m (matched pc2 point), d^2 = |q - m|^2 (the error, reference rounding),
+        //   (p - c) m^T with p the untransformed pc1 point and c = pc1[0].
+        // Then pc1_avg = T mu_p, and X Y^T = R_T [sum (p - c) m^T - dp pc2_avg^T]
+        // (q - mu_q = R_T (p - mu_p) and sum (m - pc2_avg) = 0).
+        double tot;
+        {
+            // the query point is recomputed from a re-read pc1 row (bit-identical
+            // to qx, qy) so those need not stay live through the sums
+            int tr = threadIdx.x;
+            asm volatile("" : "+v"(tr));
+            const double2 c = *reinterpret_cast<const double2*>(pconst + kPcX);
+            const double2 gmv = *reinterpret_cast<const double2*>(pconst + kGm1);
+            const double2 gsv = *reinterpret_cast<const double2*>(pconst + kGs1);
+            const double2 pcm = *reinterpret_cast<const double2*>(pconst + kPmax);   // (pmax, cmax)
+            const double bq = (fmax(fabs(T.m00) + fabs(T.m01), fabs(T.m10) + fabs(T.m11)) * pcm.x +
+                               fmax(fabs(T.m02), fabs(T.m12))) * (1.0 + 1e-12);   // >= |q|
+            const RsumGrid gm{gmv.x, gmv.y}, gs{gsv.x, gsv.y};
+            const RsumGrid gd = rsum_grid(2.0 * (bq + pcm.y) * (bq + pcm.y) * (1.0 + 1e-12), n1);
+            double acc[16];
 #pragma unroll
-        for (int k = 0; k < QPT; ++k) mk[k] = resident ? cand[bi[k]] : p2[bi[k]];
+            for (int q = 0; q < 16; ++q) acc[q] = 0.0;
 #pragma unroll
-        for (int k = 0; k < QPT; ++k) {
-            const int i = k * BLOCK + tid;
-            if (i < n1) {
-                const double2 m = mk[k];
-                v[0] += qx[k];
-                v[1] += qy[k];
-                v[2] += m.x;
-                v[3] += m.y;
-                v[4] += exact_d2(m.x, m.y, qx[k], qy[k]);   // (pc1_t - pc2[corr])**2 of the row
+            for (int k = 0; k < QPT; ++k) {
+                const int i = k * BLOCK + tr;
+                if (i < n1) {
+                    const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
+                    const double2 p = p1[i];
+                    const double x = fma(T.m02, 1.0, fma(T.m01, p.y, T.m00 * p.x));
+                    const double y = fma(T.m12, 1.0, fma(T.m11, p.y, T.m10 * p.x));
+                    rsum_add(m.x, gm, acc[0], acc[1]);
+                    rsum_add(m.y, gm, acc[2], acc[3]);
+                    rsum_add(exact_d2(m.x, m.y, x, y), gd, acc[4], acc[5]);   // (pc1_t - pc2[corr])**2
+                    const double ax = p.x - c.x, ay = p.y - c.y;
+                    rsum_add(ax * m.x, gs, acc[6], acc[7]);
+                    rsum_add(ax * m.y, gs, acc[8], acc[9]);
+                    rsum_add(ay * m.x, gs, acc[10], acc[11]);
+                    rsum_add(ay * m.y, gs, acc[12], acc[13]);
+                }
             }
+            tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
         }
-        block_sum<5, WAVES>(v, red0);
         const double n = static_cast<double>(n1);
-        const double mux = v[0] / n, muy = v[1] / n;     // pc1_avg
-        const double mvx = v[2] / n, mvy = v[3] / n;     // pc2_avg
-        const double err = v[4];
-
-        // ---- S = X @ Y.T over centred rows ------------------------------------
-        double s[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < QPT; ++k) {
-            const int i = k * BLOCK + tid;
-            if (i < n1) {
-                const double2 m = resident ? cand[bi[k]] : p2[bi[k]];   // re-read: fewer live registers
-                const double xa = qx[k] - mux, ya = qy[k] - muy;
-                const double xb = m.x - mvx, yb = m.y - mvy;
-                s[0] = fma(xa, xb, s[0]);
-                s[1] = fma(xa, yb, s[1]);
-                s[2] = fma(ya, xb, s[2]);
-                s[3] = fma(ya, yb, s[3]);
-            }
-        }
-        block_sum<4, WAVES>(s, red1);
+        const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
+        const double mvy = (readlane_d(tot, 2) + readlane_d(tot, 3)) / n;
+        const double err = readlane_d(tot, 4) + readlane_d(tot, 5);
+        const double2 dp = *reinterpret_cast<const double2*>(pconst + kDpX);
+        const double2 mup = *reinterpret_cast<const double2*>(pconst + kMupX);
+        const double mux = fma(T.m02, 1.0, fma(T.m01, mup.y, T.m00 * mup.x));   // pc1_avg = T mu_p
+        const double muy = fma(T.m12, 1.0, fma(T.m11, mup.y, T.m10 * mup.x));
+        // S_p = sum (p - mu_p)(m - pc2_avg)^T, then S = X @ Y.T = R_T S_p
+        const double p00 = fma(-dp.x, mvx, readlane_d(tot, 6) + readlane_d(tot, 7));
+        const double p01 = fma(-dp.x, mvy, readlane_d(tot, 8) + readlane_d(tot, 9));
+        const double p10 = fma(-dp.y, mvx, readlane_d(tot, 10) + readlane_d(tot, 11));
+        const double p11 = fma(-dp.y, mvy, readlane_d(tot, 12) + readlane_d(tot, 13));
+        double s[4];
+        s[0] = fma(T.m01, p10, T.m00 * p00);
+        s[1] = fma(T.m01, p11, T.m00 * p01);
+        s[2] = fma(T.m11, p10, T.m10 * p00);
+        s[3] = fma(T.m11, p11, T.m10 * p01);
 
         // ---- closed-form 2x2 Kabsch: R maximising tr(R S) ---------------------
         // Equals V diag(1, det(V U^T)) U^T of the reference's SVD route.

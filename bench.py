@@ -37,6 +37,21 @@ FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (spec), MI355X_MICROARCH.m
 FP32_VALU_PEAK_TFLOPS = 157.3    # MI355X vector FP32 (spec)
 HBM_PEAK_GBPS = 8000.0
 FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add per candidate distance
+# issue-bound candidate rate of the exact scan (~8 VALU
+# instructions per candidate): 256 CU x 2.4 GHz x 64 lanes / 8
+ISSUE_BOUND_EVALS_PER_S = 4.9e12
+KERNEL_SOURCES = ("icp-slam-with-loop-closure_amd/csrc/icp_kernels.hip", "icp-slam-with-loop-closure_amd/csrc/common.hpp")
+
+
+def kernel_source_sha():
+    """sha256 of the ICP kernel sources: ties a committed PMC profile to the
+    kernel it measured (tools/collect_profile.py records the same hash)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(REPO, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def log(*a):
@@ -199,7 +214,16 @@ def cpu_baseline(scans, inits, sample, workers):
                       f"ICP iterations): oracle/icp_oracle.py with the reference's per-query loop "
                       f"(src/icp.py:16-17), joblib loky x{workers} (scripts/main.py:240 pattern)",
             "modes": modes, "host": {"os_cpu_count": n_all, "affinity_cpus": n_aff, "workers": workers,
-                                     "cpu_model": model}}
+                                     "cpu_model": model},
+            # scripts/main.py:240 runs n_jobs=-1 (every CPU it may use).  The GPU box
+            # grants this job a 16-CPU share (OMP_NUM_THREADS; worker pools must stay
+            # within it), so `value` is n_jobs=-1 inside that share; the per-core
+            # rate scaled to every affinity CPU is an (unmeasured, linear) upper
+            # bound of the reference on the whole host
+            "projection_all_affinity_cpus": {
+                "cpus": n_aff, "pairs_per_s": round(modes["ref_loop_1_core"]["pairs_per_s"] * n_aff, 2),
+                "vectorized_pairs_per_s": round(modes["vectorized_1_core"]["pairs_per_s"] * n_aff, 2),
+                "kind": "linear projection of the 1-core rate, not measured"}}
     return base, {int(i): r for i, r in zip(idx_all, res_all)}
 
 
@@ -234,8 +258,17 @@ def pgo_bench():
         s.step(1.0 / (i + 2))
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / k
-    out = {"sgd_step_ms": round(dt * 1e3, 3), "sgd_graph": f"{len(poses)} nodes / {len(ea)} edges",
-           "sgd_ref_cpu_s_per_step": 138.9}
+    # the drop-in call scripts/main.py:325-326 makes 50 times on one graph:
+    # host poses in, one step, poses written back in place
+    import src.pose_graph_optimization as pgo_drop_in
+    pgo_drop_in.pose_graph_optimization_step_sgd(pg, learning_rate=1.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(k):
+        pgo_drop_in.pose_graph_optimization_step_sgd(pg, learning_rate=1.0 / (i + 2))
+    dt_drop = (time.perf_counter() - t0) / k
+    out = {"sgd_step_ms": round(dt * 1e3, 3), "sgd_dropin_step_ms": round(dt_drop * 1e3, 3),
+           "sgd_graph": f"{len(poses)} nodes / {len(ea)} edges", "sgd_ref_cpu_s_per_step": 138.9}
     try:
         from slamhip import gn
         out.update(gn.bench_c4())
@@ -363,17 +396,21 @@ def main():
     torch.cuda.synchronize()
     lib.slam_icp_set_eval_counter(None)
     performed = float(cnt.item())
-    peak = FP32_VALU_PEAK_TFLOPS if mode else FP64_VALU_PEAK_TFLOPS
-    flops = FLOP_PER_EVAL * performed / (kern_ms * 1e-3) / 1e12
+    evals_per_s = performed / (kern_ms * 1e-3)
+    flops = FLOP_PER_EVAL * evals_per_s / 1e12
     alg_bytes = 16.0 * float(ss.lens.sum()) + B * (4 + 4 + 72 + 72 + 8 + 4) + 8 * (len(ss.lens) + 1)
     hbm_gbps = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     valu_issue = None
     valu_per_eval = None
+    pmc_src = {"file": "profiles/pmc_traffic.json", "kernel_source_sha256": kernel_source_sha()}
     tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
+            pmc_src.update({"profile_tag": tj.get("tag"), "profile_commit": tj.get("commit"),
+                            "profile_kernel_sha256": tj.get("kernel_source_sha256")})
+            pmc_src["current"] = tj.get("kernel_source_sha256") == pmc_src["kernel_source_sha256"]
             # measured on tj["pairs"] pairs of this workload; scale to this launch
             traffic = round(tj["icp_batch_bytes_per_launch"] * B / tj.get("pairs", B))
             # VALU busy fraction of the SIMDs over the kernel's dispatches, measured
@@ -384,6 +421,11 @@ def main():
                 valu_issue = round(tj["valu_busy_frac"], 4)
             if "valu_insts_per_launch" in tj:
                 valu_per_eval = tj["valu_insts_per_launch"] * 64.0 / tj.get("pairs", B)
+            if not pmc_src["current"]:
+                # the committed counters belong to another build of the kernel:
+                # kept for reference under pmc_profile, not reported as this run's
+                pmc_src["stale_values"] = {"traffic": traffic, "valu_busy_frac": valu_issue}
+                traffic = valu_issue = valu_per_eval = None
         except Exception:
             traffic = None
     sel = lib.slam_icp_selected_instance(int(n1.max()))
@@ -409,22 +451,32 @@ def main():
                    "mean_icp_iterations": round(iters_all / pairs_all, 3),
                    "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}"},
         "roofline": {
+            # achieved = candidate evaluations per second against
+            # the VALU issue bound 4.9e12 /s (= 24.5 TFLOP/s at 5 flops each)
             "bound": "valu",
             "kernel": "slam_icp_batch_f64 (icp_kernel, %s)" % (
                 {2: "fp32 screen with exact pruning + fp64 certification",
                  1: "fp32 screen + fp64 certification", 0: "exact fp64 scan"}[mode]),
             "achieved": round(flops, 3),
-            "peak": peak,
+            "peak": round(FLOP_PER_EVAL * ISSUE_BOUND_EVALS_PER_S / 1e12, 3),
             "unit": "TFLOP/s",
-            "frac": round(flops / peak, 4),
+            "frac": round(evals_per_s / ISSUE_BOUND_EVALS_PER_S, 4),
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 4),
+            "candidate_evals_per_s": round(evals_per_s, 1),
+            "issue_bound_evals_per_s": ISSUE_BOUND_EVALS_PER_S,
+            "candidate_evals_frac_of_issue_bound": round(evals_per_s / ISSUE_BOUND_EVALS_PER_S, 4),
+            "fp64_flop_frac": round(flops / FP64_VALU_PEAK_TFLOPS, 4),
+            "fp32_flop_frac": round(flops / FP32_VALU_PEAK_TFLOPS, 4),
+            "fp64_peak_tflops": FP64_VALU_PEAK_TFLOPS,
+            "fp32_peak_tflops": FP32_VALU_PEAK_TFLOPS,
             "candidate_evals_performed_per_launch": performed,
             "brute_force_evals_per_launch": evals,
             "pruning_factor": round(evals / max(performed, 1.0), 2),
             "brute_force_equivalent_evals_per_s": round(evals / (kern_ms * 1e-3), 1),
             "valu_busy_frac": valu_issue,
             "valu_busy_source": "profiles/pmc_traffic.json (rocprofv3 SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE, C3 batch)",
+            "pmc_profile": pmc_src,
             "valu_lane_insts_per_candidate_eval": (round(valu_per_eval * B / performed, 2)
                                                    if valu_per_eval and performed else None),
             "brute_force_equivalent_note": "pruning skips candidates exactly; the brute-force-equivalent rate is "

@@ -424,8 +424,11 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
         // (which consumed the reads); only the owner of b waits for the count
         // (normally already complete), the other threads go on.  Release (every
         // lane's reads of P ordered before the count) / acquire (the owner's
-        // write of P[b] ordered after it), workgroup scope.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // write of P[b] ordered after it), workgroup scope; with P in LDS the
+        // fence covers LDS only (it does not wait for the next edge's
+        // prefetched global operands)
+        if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if ((tid & 63) == 0) __hip_atomic_fetch_add(&rd_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint32_t rd_target = static_cast<uint32_t>(kRelaxBlock / 64) * static_cast<uint32_t>(k + 1);
         // ---- explicit nodes (a's block remainder, b's block) ----------------------
@@ -435,8 +438,10 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             double cij[3] = {cur.ci[0], cur.ci[1], cur.ci[2]};
             while (i >= 0) {
                 if (i == b) {
-                    while (__hip_atomic_load(&rd_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < rd_target)
+                    while (__hip_atomic_load(&rd_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < rd_target)
                         __builtin_amdgcn_s_sleep(1);
+                    if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
                 if (i <= b) {
 #pragma unroll

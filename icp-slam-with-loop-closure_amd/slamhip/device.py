@@ -28,6 +28,8 @@ def to_dev(a, dtype, device=None):
     t = require_gpu()
     dev = device if device is not None else default_device()
     arr = np.ascontiguousarray(a, dtype=dtype)
+    if not arr.flags.writeable:   # e.g. PoseGraph's cached edge arrays (torch wants writable memory)
+        arr = arr.copy()
     return t.from_numpy(arr).to(dev, non_blocking=False)
 
 

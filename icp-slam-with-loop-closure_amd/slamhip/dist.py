@@ -64,6 +64,8 @@ def sharded_chain(odometry0, tf_local, n_items, group=None, iters_local=None, er
     err = torch.as_tensor(np.zeros(B) if err_local is None else np.asarray(err_local, dtype=np.float64))
     its = torch.as_tensor(np.zeros(B, np.int64) if iters_local is None else np.asarray(iters_local))
     local = pack(tf, err, its, max(per, 1))
+    if dist.get_backend(group) != "gloo":   # RCCL gathers device tensors only
+        local = local.to(torch.device("cuda", torch.cuda.current_device()))
     g = all_gather_results(local, group)
     tf_all, err_all, it_all = unpack(g, n_items)
     return se2.compose_chain(np.asarray(odometry0, dtype=np.float64), tf_all), tf_all, err_all, it_all

@@ -161,6 +161,15 @@ class GaussNewton:
                     break
             self.chi2 = np.asarray(out)
             return self.chi2
+        if stream is not None:
+            # every torch op of the run (status reset, chi2 buffer, read-backs)
+            # on the caller's stream, ordered with the launches
+            with t.cuda.stream(stream):
+                return self._run(iterations, stream, False)
+        return self._run(iterations, None, graph)
+
+    def _run(self, iterations, stream, graph):
+        t = dv.torch()
         self.status.zero_()   # a failed earlier run must not poison this one
         if graph is None:
             graph = self._eager_done and stream is None and iterations > 0

@@ -33,6 +33,11 @@ class SgdSolver:
             float(learning_rate), float(loop_closure_uncertainty), dv.ptr(self.work),
             dv.stream_handle(stream)), "slam_pgo_sgd_step_f64")
 
+    def set_poses(self, poses):
+        """Upload new (N, 3) poses into the resident buffer (same graph)."""
+        p = np.ascontiguousarray(poses, dtype=np.float64).reshape(self.poses.shape)
+        self.poses.copy_(dv.torch().from_numpy(p.copy() if not p.flags.writeable else p))
+
     def orient(self, stream=None):
         _abi.check(_abi.lib().slam_pgo_orient_f64(dv.ptr(self.poses), self.N, dv.stream_handle(stream)),
                    "slam_pgo_orient_f64")

@@ -84,8 +84,18 @@ def manual_loop_closures(pg, lidar_points, matches, max_iters=100, epsilon=0.05,
     ok = r.err < err_thresh
     for (i, j), t, good in zip(matches, r.tf, ok):
         if good:
-            pg.add_constraint(int(i), int(j), t.copy())
+            add_loop_constraint(pg, int(i), int(j), t.copy(), "icp")   # icp(pc_i, pc_j): X_i = X_j T
     return ok
+
+
+def add_loop_constraint(pg, i, j, T, convention):
+    """``pg.add_constraint(i, j, T)`` recording the measurement convention
+    (src/pose_graph.py) when the graph type supports it — the reference's
+    own PoseGraph (or any duck-typed graph) gets the plain call."""
+    try:
+        pg.add_constraint(i, j, T, convention=convention)
+    except TypeError:
+        pg.add_constraint(i, j, T)
 
 
 def optimize(pg, lidar_points, optimization_max_iters=50, icp_max_iters=100, icp_epsilon=0.05,

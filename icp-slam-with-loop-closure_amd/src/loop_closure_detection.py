@@ -24,6 +24,7 @@ import numpy as np
 import scipy.spatial
 
 from slamhip import icp as _k
+from slamhip.pipeline import add_loop_constraint
 
 
 def _cv2():
@@ -75,7 +76,8 @@ def detect_proximity(pose_graph, lidar_points, min_dist_along_path=2, max_dist=1
         error = float(res.err[b])
         if error < err_thresh:
             print("%d %d %f" % (i, j, error))
-            pose_graph.add_constraint(i, j, res.tf[b].copy())
+            # icp(pc_j, pc_i): X_j = X_i T, the "relative" convention (src/pose_graph.py)
+            add_loop_constraint(pose_graph, i, j, res.tf[b].copy(), "relative")
             used.update((i, j))
 
 
@@ -164,7 +166,7 @@ def detect_images_direct_similarity(pose_graph, lidar_points, images, image_rate
     for b, (i0, j0) in enumerate(good):
         i, j = i0 * image_rate, j0 * image_rate
         if float(res.err[b]) < icp_err_thresh:
-            pose_graph.add_constraint(i, j, res.tf[b].copy())
+            add_loop_constraint(pose_graph, i, j, res.tf[b].copy(), "icp")   # icp(pc_i, pc_j): X_i = X_j T
             if save_matches:
                 img = cv2.drawMatches(greys[i], keypoints[i0], greys[j], keypoints[j0], matched.get((i0, j0), []), None,
                                       flags=cv2.DrawMatchesFlags_NOT_DRAW_SINGLE_POINTS)

@@ -24,9 +24,25 @@ from slamhip.se2 import pose_to_mat
 
 
 def pose_graph_optimization_step_sgd(pose_graph, learning_rate=1, loop_closure_uncertainty=0.1):
-    ea, eb, tf = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
-    out = _pgo.sgd_step(pose_graph.poses, ea, eb, tf, learning_rate, loop_closure_uncertainty)
-    pose_graph.poses[...] = out
+    """Reference :7-49.  The flattened edges (``PoseGraph.edge_arrays``, cached
+    until the graph changes) and their device copy plus the step's scratch are
+    kept on the graph object between calls (scripts/main.py:325-326 runs 50
+    steps on one graph): a call uploads the poses, runs the step and writes
+    them back in place."""
+    flat = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
+    cache = getattr(pose_graph, "_sgd_solver", None)
+    N = len(pose_graph.poses)
+    if cache is None or cache[0] is not flat or cache[1].N != N:
+        cache = (flat, _pgo.SgdSolver(pose_graph.poses, *flat))
+        try:
+            pose_graph._sgd_solver = cache
+        except AttributeError:   # a graph type without attribute storage: no cache
+            pass
+    else:
+        cache[1].set_poses(pose_graph.poses)
+    s = cache[1]
+    s.step(learning_rate, loop_closure_uncertainty)
+    pose_graph.poses[...] = s.host_poses()
 
 
 def recompute_pose_graph_orientation(pose_graph, lidar_points, icp_max_iters, icp_epsilon, n_jobs,
@@ -73,31 +89,49 @@ def optimize_pose_graph(pose_graph, iterations=10, odom_information=2.0, loop_in
 def gn_measurements(pose_graph, odometry_edges="global_delta", loop_edges="icp"):
     """(ea, eb, z (E, 3, 3)) in networkx edge order with X_b = X_a z for every edge.
 
-    A constructor odometry edge (a, a+1) holds odom_change_to_mat(P[a+1] - P[a]):
-    rotation by the heading change and the GLOBAL translation delta; its
-    relative measurement is R(theta_a)^T delta with theta_a the heading the
-    delta was taken at (``PoseGraph.odometry_headings``; the current pose's
-    heading for graphs without it, e.g. loaded from a pickle before
-    optimisation, as scripts/main.py saves them)."""
+    Each edge is classified by what ``PoseGraph`` recorded when it was added
+    (``PoseGraph.edge_kinds``):
+
+    * a constructor edge (a, a+1) holds odom_change_to_mat(P[a+1] - P[a]):
+      rotation by the heading change and the GLOBAL translation delta; its
+      relative measurement is R(theta_a)^T delta with theta_a the heading the
+      delta was taken at (the edge's ``heading``) — ``odometry_edges=
+      "relative"`` keeps such edges as they are;
+    * a constraint added with ``convention="icp"`` (X_a = X_b T: icp(pc_a,
+      pc_b), the manual / image loop closures) is inverted; one added with
+      ``convention="relative"`` (icp(pc_b, pc_a), ``detect_proximity``) is kept;
+    * a constraint without a recorded convention follows ``loop_edges``.
+
+    A graph with no annotations at all (built by the reference's own
+    PoseGraph, or a reference pickle) falls back to the shape rule: (a, a+1)
+    edges are constructor deltas at the current pose's heading, the others
+    follow ``loop_edges``."""
     if odometry_edges not in ("global_delta", "relative") or loop_edges not in ("icp", "relative"):
         raise ValueError("odometry_edges in {global_delta, relative}, loop_edges in {icp, relative}")
     ea, eb, tf = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
     z = np.array(tf, dtype=np.float64).reshape(-1, 3, 3)
-    odo = eb.astype(np.int64) == ea.astype(np.int64) + 1
-    if odometry_edges == "global_delta" and odo.any():
-        known = getattr(pose_graph, "odometry_headings", {}) or {}
-        th = np.array([known.get(int(a), pose_graph.poses[int(a), 2]) for a in ea[odo]], dtype=np.float64)
+    if hasattr(pose_graph, "edge_kinds"):
+        head, conv = pose_graph.edge_kinds()
+    else:
+        head, conv = np.full(len(ea), np.nan), np.zeros(len(ea), np.int8)
+    delta = ~np.isnan(head)
+    if not delta.any() and not conv.any():   # unannotated graph: the shape rule
+        delta = eb.astype(np.int64) == ea.astype(np.int64) + 1
+        head = np.where(delta, np.asarray(pose_graph.poses, dtype=np.float64)[ea, 2], np.nan)
+    if odometry_edges == "global_delta" and delta.any():
+        th = head[delta]
         c, s = np.cos(th), np.sin(th)
-        dx, dy = z[odo, 0, 2].copy(), z[odo, 1, 2].copy()
-        z[odo, 0, 2] = c * dx + s * dy
-        z[odo, 1, 2] = -s * dx + c * dy
-    if loop_edges == "icp" and (~odo).any():
-        r = z[~odo]
+        dx, dy = z[delta, 0, 2].copy(), z[delta, 1, 2].copy()
+        z[delta, 0, 2] = c * dx + s * dy
+        z[delta, 1, 2] = -s * dx + c * dy
+    invert = ~delta & ((conv == 1) | ((conv == 0) & (loop_edges == "icp")))
+    if invert.any():
+        r = z[invert]
         inv = np.zeros_like(r)
         inv[:, :2, :2] = np.transpose(r[:, :2, :2], (0, 2, 1))        # R^T
         inv[:, :2, 2] = -np.einsum("eij,ej->ei", inv[:, :2, :2], r[:, :2, 2])
         inv[:, 2, 2] = 1.0
-        z[~odo] = inv
+        z[invert] = inv
     return ea, eb, z
 
 

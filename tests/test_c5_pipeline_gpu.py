@@ -8,8 +8,9 @@ reference's flow (scripts/main.py:236-339) restated with the CPU oracle:
 * stage 3: 50 SGD steps (lr = 1/(k+1)) + the orientation recompute;
 * the final occupancy map of a subset of scans vs oracle/occupancy_oracle.
 
-3,000 scans of 181 beams keep the oracle's flow within about a minute (the
-full 50k x 1081 run is tools/c5_pipeline.py; same code path, larger arrays).
+The first test runs the WHOLE oracle flow on 3,000 scans of 181 beams (within
+about a minute); the second runs C5 at its real shape (50,000 x 1081) with
+sampled oracle checks (tools/c5_pipeline.py; same code path).
 Positions within 1e-9, headings within 1e-9 (compared raw, not modulo 2 pi:
 the orientation recompute leaves atan2-range headings), map cells equal.
 """
@@ -84,3 +85,28 @@ def test_c5_shape_pipeline_vs_oracle():
     gl = [dev_g[offs[i]:offs[i + 1]] for i in range(len(subscans))]
     rgrid = oo.update(np.zeros_like(grid), pg.poses[sub], subscans, 0.05, origin[0], origin[1], gpts=gl)
     assert np.array_equal(grid, rgrid)
+
+
+def test_c5_full_shape_50k_scans():
+    """Config C5 at its real shape: 50,000 scans x 1081 beams (synthetic
+    indoor loop, ~4,950 ground-truth loop pairs) through the whole flow of
+    tools/c5_pipeline.py — stage 1 batched ICP over 49,999 pairs, the manual
+    loop closures in one launch, 50 SGD steps + orientation recompute on the
+    50k-node graph, the occupancy map — with bounded CPU-oracle checks (the
+    full CPU flow takes hours): 24 sampled stage-1 pairs and 16 loop pairs
+    (transforms within 1e-9), the first 2 SGD steps on the full graph
+    (positions within 1e-9) and the map of the first scans (cells equal)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import c5_pipeline
+    rep = c5_pipeline.run(50000, 2)
+    assert rep["scans"] == 50000 and rep["loop_pairs"] > 4000
+    assert rep["loop_closures_accepted"] > 0.9 * rep["loop_pairs"]
+    assert rep["check_stage1_pairs"]["max_abs_tf_diff"] <= TOL
+    assert rep["check_loop_pairs"]["max_abs_tf_diff"] <= TOL
+    assert rep["check_sgd"]["max_abs_xy_diff"] <= TOL
+    m = rep["check_map"]
+    assert m["points_within_4ulp"] and m["origin_within_1e-12"] and m["grid_identical"]
+    # the loop closures pull the trajectory back towards the truth
+    assert rep["drift_vs_truth_after_m"] < rep["drift_vs_truth_before_m"]

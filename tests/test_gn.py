@@ -255,6 +255,96 @@ def test_gn_measurements_of_a_consistent_graph_have_zero_chi2():
     assert np.allclose(pgo.gn_measurements(q)[2], z, atol=1e-15)
 
 
+def test_gn_measurements_follow_recorded_conventions(tmp_path):
+    """Each constraint is converted by the convention recorded when it was
+    added: "icp" (X_a = X_b T, the manual / image closures), "relative"
+    (X_b = X_a T, detect_proximity's icp(pc_j, pc_i)), an overwritten
+    constructor edge stops being a global delta, and the annotations survive
+    the reference's (poses, DiGraph) pickle: chi2 = 0 at the true poses."""
+    import src.pose_graph as pgm
+    import src.pose_graph_optimization as pgo
+    from slamhip import se2, synthetic
+    s = synthetic.make_loop_sequence(400, seed=3, n_beams=31)
+    X = [se2.pose_to_mat(p) for p in s.truth]
+    pg = pgm.PoseGraph(s.truth.copy())
+    for k, (a, b) in enumerate(s.loop_pairs):
+        a, b = int(a), int(b)
+        if k % 2:
+            pg.add_constraint(a, b, np.linalg.inv(X[b]) @ X[a], convention="icp")
+        else:
+            pg.add_constraint(a, b, np.linalg.inv(X[a]) @ X[b], convention="relative")
+    pg.add_constraint(7, 8, np.linalg.inv(X[7]) @ X[8], convention="relative")   # overwrites a constructor edge
+
+    def chi2(g):
+        ea, eb, z = pgo.gn_measurements(g)
+        return go.build_system(s.truth.copy(), ea.astype(np.int64), eb.astype(np.int64),
+                               go.edge_measurements(z), go.information(ea, eb))[3]
+    assert chi2(pg) < 1e-20
+    f = str(tmp_path / "g.pickle")
+    pg.save(f)
+    q = pgm.PoseGraph(None)
+    q.load(f)
+    assert chi2(q) < 1e-20
+    # the default for unrecorded constraints is loop_edges ("icp"): the relative ones are then wrong
+    r = pgm.PoseGraph(s.truth.copy())
+    for a, b in s.loop_pairs[:4]:
+        r.add_constraint(int(a), int(b), np.linalg.inv(X[int(a)]) @ X[int(b)])
+    ea, eb, z = pgo.gn_measurements(r, loop_edges="relative")
+    assert go.build_system(s.truth.copy(), ea.astype(np.int64), eb.astype(np.int64), go.edge_measurements(z),
+                           go.information(ea, eb))[3] < 1e-20
+    with pytest.raises(ValueError):
+        pg.add_constraint(0, 5, np.eye(3), convention="global")
+
+
+def test_edge_arrays_cache_follows_the_graph():
+    """PoseGraph.edge_arrays() is cached between SGD calls and rebuilt after
+    add_constraint / flip / load or a direct change of the graph."""
+    import src.pose_graph as pgm
+    poses = np.c_[np.arange(6.0), np.zeros(6), np.zeros(6)]
+    pg = pgm.PoseGraph(poses)
+    a = pg.edge_arrays()
+    assert pg.edge_arrays() is a and not a[2].flags.writeable
+    pg.add_constraint(0, 4, np.eye(3))
+    b = pg.edge_arrays()
+    assert b is not a and len(b[0]) == 6
+    pg.graph.add_edge(1, 5, object=np.eye(3))    # behind the class's back
+    assert len(pg.edge_arrays()[0]) == 7
+    c = pg.edge_arrays()
+    pg.flip()
+    d = pg.edge_arrays()
+    assert d is not c and sorted(zip(d[0].tolist(), d[1].tolist())) == sorted((5 - b, 5 - a) for a, b in
+                                                                             zip(c[0].tolist(), c[1].tolist()))
+
+
+@pytest.mark.gpu
+def test_detect_proximity_edges_feed_gn_consistently():
+    """detect_proximity (icp(pc_j, pc_i), X_j = X_i T) followed by
+    gn_measurements: at the true poses the loop residuals are ICP-accurate
+    (cm) — the inverted reading of the same edges is off by twice the pairs'
+    offsets (laps ~0.3 m apart)."""
+    import src.loop_closure_detection as lcd
+    import src.pose_graph as pgm
+    import src.pose_graph_optimization as pgo
+    from slamhip import synthetic
+    # laps 0.3 m apart (lap_jitter): the proximity pairs' offsets dwarf ICP's cm errors
+    s = synthetic.make_loop_sequence(1200, seed=3, n_beams=361, lap_jitter=0.3)   # pairs ~0.3 m apart
+    pg = pgm.PoseGraph(s.truth.copy())
+    lcd.detect_proximity(pg, s.scans, min_dist_along_path=2, max_dist=1, err_thresh=110)
+    ea, eb, z = pgo.gn_measurements(pg)
+    loop = eb != ea + 1
+    assert loop.sum() > 3
+    def loop_res(zz):
+        e, _, _ = go.linearize(s.truth.copy(), ea.astype(np.int64), eb.astype(np.int64), go.edge_measurements(zz),
+                               go.information(ea, eb))
+        return np.hypot(e[loop][:, 0], e[loop][:, 1])
+    inv = z.copy()
+    inv[loop] = np.linalg.inv(z[loop])
+    good, bad = loop_res(z), loop_res(inv)
+    assert np.median(good) < 0.03 and np.median(bad) > 5 * np.median(good), (np.median(good), np.median(bad))
+    same = pgo.gn_measurements(pg, loop_edges="icp")[2]   # unchanged: the edges carry their convention
+    assert np.array_equal(same, z)
+
+
 @pytest.mark.gpu
 def test_pipeline_gn_reduces_drift():
     """The batched driver's GN path (scan matching -> PoseGraph -> manual loop

@@ -20,9 +20,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "icp-slam-with-loop-closure_amd"), os.path.join(REPO, "oracle")]
 
 
-def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
-    sgd_check = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+def run(n=50000, sgd_check=2, seed=7):
+    """The whole C5 flow on n scans; returns the report dict (tests/test_c5_pipeline_gpu.py)."""
     import torch
     import icp_oracle
     import pgo_oracle as po
@@ -30,10 +29,10 @@ def main():
     from slamhip import icp as k
     from slamhip import pgo, pipeline, se2, synthetic
     t0 = time.perf_counter()
-    seq = synthetic.make_loop_sequence(n, seed=7)
+    seq = synthetic.make_loop_sequence(n, seed=seed)
     t_gen = time.perf_counter() - t0
     print(f"generated {n} scans in {t_gen:.1f}s", file=sys.stderr, flush=True)
-    rep = {"config": "C5 stand-in: synthetic indoor loop (seed 7), ground-truth manual loop closures",
+    rep = {"config": f"C5 stand-in: synthetic indoor loop (seed {seed}), ground-truth manual loop closures",
            "scans": n, "per_lap": seq.per_lap, "loop_pairs": int(len(seq.loop_pairs))}
     pipeline.scan_matching(seq.odometry[:3], seq.scans[:3])     # warm-up
     torch.cuda.synchronize()
@@ -119,7 +118,14 @@ def main():
     rep["check_map"] = {"scans": 6, "points_within_4ulp": pts_ok, "origin_within_1e-12": bool(org_ok),
                         "grid_identical": bool(np.array_equal(g_gpu, rgrid)),
                         "note": "GPU map vs oracle/occupancy_oracle.py (per-beam restatement) on the first scans"}
-    print(json.dumps(rep))
+    rep["generate_s"] = round(t_gen, 2)
+    return rep
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
+    sgd_check = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    print(json.dumps(run(n, sgd_check)))
 
 
 if __name__ == "__main__":

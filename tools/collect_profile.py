@@ -63,6 +63,16 @@ def main(tag):
            "workload": "tools/prof_icp.py 10000 pairs x 1081 pts, one batch (both scheduler phases summed)", "pairs": 10000,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH x2 (gfx950)",
            "tag": tag}
+    # tie the counters to the kernel build they measured (bench.py compares the hash)
+    sys.path.insert(0, REPO)
+    import bench
+    out["kernel_source_sha256"] = bench.kernel_source_sha()
+    try:
+        import subprocess
+        out["commit"] = subprocess.run(["git", "-C", REPO, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                       text=True, check=True).stdout.strip()
+    except Exception:
+        out["commit"] = None
     if "SQ_INSTS_VALU" in vals:
         out.update({"valu_insts_per_launch": vals["SQ_INSTS_VALU"], "salu_insts_per_launch": vals["SQ_INSTS_SALU"],
                     "lds_insts_per_launch": vals["SQ_INSTS_LDS"], "waves_per_launch": vals["SQ_WAVES"],

@@ -5,7 +5,7 @@
 #   separate passes; FETCH_SIZE under-reports wide coalesced reads by 2x), then
 #   the instruction mix (VALU / SALU / LDS instructions, waves).
 set -e
-TAG=${1:-r01}
+TAG=${1:-r03}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT

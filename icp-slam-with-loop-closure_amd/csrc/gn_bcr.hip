@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <type_traits>
 
@@ -544,6 +545,423 @@ __global__ __launch_bounds__(kBcrThreads) void bcr_back_kernel(const double* __r
     }
 }
 
+// ---------------------------------------------------------------------------
+// MFMA path (default): blocked right-looking elimination in 16-column panels,
+// the dense trailing and right-hand-side updates and the even blocks' Schur
+// products on v_mfma_f64_16x16x4_f64.
+// ---------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// gfx950 v_mfma_f64_16x16x4_f64 (cdna_hip_programming.md, MFMA fragment
+// layout): lane l holds A[row l & 15][k l >> 4] and B[k l >> 4][col l & 15];
+// element g of the C/D tile is (row (l >> 4) + 4 g, col l & 15).
+__device__ __forceinline__ f64x4 mfma16(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int T>
+struct BcrMfmaLds {
+    static constexpr int WB = 16 * T;
+    static constexpr int LDA = WB + 1;              // A: [WB][LDA] (odd stride: spread banks)
+    static constexpr int LDZ = 16 * (T + 1) + 1;    // panel rows of the right-hand side, x2 buffers
+    static constexpr size_t doubles = static_cast<size_t>(WB) * LDA + 2 * 16 * LDZ + 2 * WB + 32;   // + rdg, y, 2 columns
+    static constexpr size_t bytes = doubles * sizeof(double);
+};
+
+// D_i (WB x WB, global, row-major) -> A (LDS): every load in flight at once.
+template <int T>
+__device__ __forceinline__ void bcr_stage_block(const double* __restrict__ src, double* A) {
+    constexpr int WB = 16 * T, LDA = WB + 1, PER = WB * WB / kBcrThreads;
+    double g[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) g[q] = src[threadIdx.x + kBcrThreads * q];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + kBcrThreads * q;
+        A[(e / WB) * LDA + e % WB] = g[q];
+    }
+}
+
+// Cholesky D = C C^T of the block in LDS (A; lower triangle read) and the
+// forward substitution Z = C^-1 R of NR (<= T + 1) 16-column right-hand-side
+// tiles, blocked in T panels of 16 columns.  Per panel p:
+//   F(p)   wave 0: rows 16p.. x 16 columns factored in registers, the pivot
+//          and L[c][k] broadcast by v_readlane: no barrier inside the panel;
+//   UR(p-1) waves 1-3, beside F(p): R_i -= L_i,p-1 Z_p-1 on their register-
+//          resident R tiles (MFMA), the tiles of panel p's rows then to LDS;
+//   --- barrier ---
+//   S(p)   waves 1-2: Z_p = L_pp^-1 R_p, one thread per right-hand-side column;
+//   UA(p)  waves 0, 3: A_ij -= L_ip L_jp^T on the lower tiles (MFMA);
+//   --- barrier ---
+// 2T barriers per block instead of one per pivot (16T).  rinit(row, col) is R,
+// out(row, col, z) receives Z; rdg[k] = 1 / C[k][k].  Returns "a pivot was not
+// positive" (wave-uniform in wave 0).
+#ifdef SLAM_BCR_STAMPS
+// tools/bcr_ubench.hip: per wave, cycles in [P1 work, barrier 1, P2 work, barrier 2]
+__device__ unsigned long long g_bcr_stamps[4][4];
+#define BCR_STAMP(q)                                                                     \
+    do {                                                                                 \
+        const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                    \
+        if (blockIdx.x == 0 && blockIdx.y == 0 && lane == 0) g_bcr_stamps[wave][q] += t1_ - t0_; \
+        t0_ = t1_;                                                                       \
+    } while (0)
+#else
+#define BCR_STAMP(q) (void)0
+#endif
+
+template <int T, typename RInit, typename Out>
+__device__ bool bcr_blocked_elim(double* A, double* Zb, double* rdg, int NR, RInit rinit, Out out) {
+    constexpr int WB = 16 * T, LDA = WB + 1, LDZ = 16 * (T + 1) + 1;
+    constexpr int MAXS = (T * (T + 1) + 2) / 3;   // R tiles per wave (waves 1-3)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lk = lane >> 4;
+#ifdef SLAM_BCR_STAMPS
+    unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+#endif
+    f64x4 racc[MAXS];
+    if (wave > 0) {
+#pragma unroll
+        for (int s = 0; s < MAXS; ++s) {
+            const int t = 3 * s + wave - 1;
+            if (t < T * NR) {
+                const int ti = t / NR, w = t % NR;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) racc[s][g] = rinit(16 * ti + lk + 4 * g, 16 * w + lr);
+                if (ti == 0) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Zb[(lk + 4 * g) * LDZ + 16 * w + lr] = racc[s][g];
+                }
+            }
+        }
+    }
+    __syncthreads();   // A staged by the caller, R_0 in Zb[0]
+#ifdef SLAM_BCR_STAMPS
+    t0_ = __builtin_amdgcn_s_memtime();
+#endif
+    bool bad = false;
+#pragma unroll
+    for (int p = 0; p < T; ++p) {
+        double* Zc = Zb + (p & 1) * 16 * LDZ;          // R_p (then Z_p)
+        double* Zp = Zb + ((p + 1) & 1) * 16 * LDZ;    // Z_p-1
+        if (wave == 0) {
+            // ---- F(p) --------------------------------------------------------
+            const int r0 = 16 * p + lane, r1 = 16 * p + 64 + lane;
+            const bool v0 = r0 < WB, v1 = (WB - 16 * p > 64) && r1 < WB;
+            double a[16], b[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                a[c] = v0 ? A[r0 * LDA + 16 * p + c] : 0.0;
+                b[c] = v1 ? A[r1 * LDA + 16 * p + c] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const double piv = readlane_d(a[k], k);
+                bad |= !(piv > 0.0);
+#ifdef SLAM_F_FAST
+                // v_rsq_f64 and one Newton step (relative error ~2^-57)
+                const double y0 = __builtin_amdgcn_rsq(piv);
+                const double rd = fma(0.5 * y0, fma(-piv * y0, y0, 1.0), y0);
+#else
+                const double rd = rsqrt(piv);   // reciprocal pivot: no fp64 division on the chain
+#endif
+                const double lk0 = a[k] * rd, lk1 = b[k] * rd;
+#ifdef SLAM_F_LDS
+                // column k of the diagonal block through LDS (one write, broadcast reads)
+                double* colk = Zb + 2 * 16 * LDZ + 2 * WB + (k & 1) * 16;
+                if (lane < 16) colk[lane] = lk0;
+#pragma unroll
+                for (int c = k + 1; c < 16; ++c) {
+                    const double lc = colk[c];
+                    a[c] = fma(-lk0, lc, a[c]);
+                    b[c] = fma(-lk1, lc, b[c]);
+                }
+#else
+#pragma unroll
+                for (int c = k + 1; c < 16; ++c) {
+                    const double lc = readlane_d(lk0, c);   // L[16p + c][16p + k]
+                    a[c] = fma(-lk0, lc, a[c]);
+                    b[c] = fma(-lk1, lc, b[c]);
+                }
+#endif
+                a[k] = lane > k ? lk0 : (lane == k ? piv * rd : a[k]);
+                b[k] = lk1;
+                if (lane == k) rdg[16 * p + k] = rd;
+            }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                if (v0) A[r0 * LDA + 16 * p + c] = a[c];
+                if (v1) A[r1 * LDA + 16 * p + c] = b[c];
+            }
+        } else if (p > 0) {
+            // ---- UR(p-1) -----------------------------------------------------
+#pragma unroll
+            for (int s = 0; s < MAXS; ++s) {
+                const int t = 3 * s + wave - 1;
+                if (t < T * NR) {
+                    const int ti = t / NR, w = t % NR;
+                    if (ti >= p) {
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) {
+                            const double av = -A[(16 * ti + lr) * LDA + 16 * (p - 1) + 4 * kk + lk];
+                            const double bv = Zp[(4 * kk + lk) * LDZ + 16 * w + lr];
+                            racc[s] = mfma16(av, bv, racc[s]);
+                        }
+                        if (ti == p) {
+#pragma unroll
+                            for (int g = 0; g < 4; ++g) Zc[(lk + 4 * g) * LDZ + 16 * w + lr] = racc[s][g];
+                        }
+                    }
+                }
+            }
+        }
+        BCR_STAMP(0);
+        __syncthreads();
+        BCR_STAMP(1);
+        if (wave == 1 || wave == 2) {
+            // ---- S(p): one right-hand-side column per thread ----------------------
+            const int c = tid - 64;
+            if (c < 16 * NR) {
+                double z[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) z[r] = Zc[r * LDZ + c];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const double zk = z[k] * rdg[16 * p + k];
+                    z[k] = zk;
+#pragma unroll
+                    for (int r = k + 1; r < 16; ++r) z[r] = fma(-A[(16 * p + r) * LDA + 16 * p + k], zk, z[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    Zc[r * LDZ + c] = z[r];
+                    out(16 * p + r, c, z[r]);
+                }
+            }
+        } else {
+            // ---- UA(p): lower tiles (ti, tj), p < tj <= ti, alternating waves 0 / 3
+            int idx = 0;
+#pragma unroll
+            for (int ti = p + 1; ti < T; ++ti) {
+#pragma unroll
+                for (int tj = p + 1; tj <= ti; ++tj, ++idx) {
+                    if ((idx & 1) != (wave == 3 ? 1 : 0)) continue;
+                    f64x4 cc;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) cc[g] = A[(16 * ti + lk + 4 * g) * LDA + 16 * tj + lr];
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const double av = -A[(16 * ti + lr) * LDA + 16 * p + 4 * kk + lk];
+                        const double bv = A[(16 * tj + lr) * LDA + 16 * p + 4 * kk + lk];
+                        cc = mfma16(av, bv, cc);
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) A[(16 * ti + lk + 4 * g) * LDA + 16 * tj + lr] = cc[g];
+                }
+            }
+        }
+        BCR_STAMP(2);
+        __syncthreads();
+        BCR_STAMP(3);
+    }
+    return bad;
+}
+
+// Odd blocks of level s, three workgroups per block (blockIdx.y = q), each
+// eliminating D_i with one set of right-hand sides: q 0: E_p (-> X_i),
+// q 1: [E_i^T | b_i] (-> Y_i, z_i), q 2: the identity (-> C_i^-1, for the
+// back-substitution).
+template <int T>
+__global__ __launch_bounds__(kBcrThreads) void bcr_odd_mfma_kernel(const double* __restrict__ D,
+                                                                   const double* __restrict__ E,
+                                                                   double* __restrict__ Cs, double* __restrict__ Xs,
+                                                                   double* __restrict__ Ys, double* __restrict__ bz,
+                                                                   int32_t Wb, int32_t nb, int32_t s,
+                                                                   int32_t* __restrict__ status) {
+    using L = BcrMfmaLds<T>;
+    constexpr int WB = L::WB;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* A = lds;
+    double* Zb = A + WB * L::LDA;
+    double* rdg = Zb + 2 * 16 * L::LDZ;
+    const int q = blockIdx.y;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const int64_t B2 = bcr_blk(WB);
+    const double* Ep = E + p * B2;   // A[i, p]
+    const double* Ei = E + i * B2;   // A[n, i]; A[i, n] = its transpose
+    const bool hn = n < nb;
+    bcr_stage_block<T>(D + i * B2, A);
+    double* Out = (q == 0 ? Xs : q == 1 ? Ys : Cs) + i * B2;
+    double* bzi = bz + static_cast<int64_t>(i) * WB;
+    auto rinit = [&](int row, int col) -> double {
+        if (q == 0) return Ep[row * WB + col];
+        if (q == 2) return row == col ? 1.0 : 0.0;
+        if (col < WB) return hn ? Ei[col * WB + row] : 0.0;
+        return col == WB ? bzi[row] : 0.0;
+    };
+    auto out = [&](int row, int col, double v) {
+        if (col < WB) Out[row * WB + col] = v;
+        else if (col == WB) bzi[row] = v;
+    };
+    const bool bad = bcr_blocked_elim<T>(A, Zb, rdg, q == 1 ? T + 1 : T, rinit, out);
+    if (bad && q == 1 && threadIdx.x == 0) *status = 1;
+}
+
+// Even blocks of level s: the two factors a workgroup needs are staged in LDS
+// once (coalesced, every load in flight), then each wave computes one 16 x 16
+// output tile with K = WB on MFMA, its operands read from LDS up front:
+//   D workgroups (y < nD):  lower tiles of D_j -= Y1^T Y1 + X2^T X2, and the
+//                           wave after the last tile b_j -= Y1^T z1 + X2^T z2
+//                           (i1 = j - s, i2 = j + s);
+//   E workgroups (y >= nD): E'_j = -Y2^T X2 (the new coupling to j + 2s).
+// (Only D_j's lower triangle is kept current: every reader uses that half.)
+template <int T>
+__device__ __forceinline__ f64x4 bcr_tile_atb(const double* La, const double* Lb, int ti, int tj, f64x4 c) {
+    // c += (La^T Lb)[16ti.., 16tj..] for La, Lb [WB][WB + 1] in LDS
+    constexpr int WB = 16 * T, LD = WB + 1;
+    const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+    double av[WB / 4], bv[WB / 4];
+#pragma unroll
+    for (int k4 = 0; k4 < WB / 4; ++k4) {
+        av[k4] = La[(4 * k4 + lk) * LD + 16 * ti + lr];
+        bv[k4] = Lb[(4 * k4 + lk) * LD + 16 * tj + lr];
+    }
+#pragma unroll
+    for (int k4 = 0; k4 < WB / 4; ++k4) c = mfma16(av[k4], bv[k4], c);
+    return c;
+}
+
+template <int T>
+__device__ __forceinline__ void bcr_stage_pair(const double* __restrict__ s1, const double* __restrict__ s2,
+                                               double* L1, double* L2) {
+    constexpr int WB = 16 * T, LD = WB + 1, PER = WB * WB / kBcrThreads;
+    double g1[PER], g2[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + kBcrThreads * q;
+        g1[q] = s1 ? s1[e] : 0.0;
+        g2[q] = s2 ? s2[e] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + kBcrThreads * q;
+        L1[(e / WB) * LD + e % WB] = g1[q];
+        L2[(e / WB) * LD + e % WB] = g2[q];
+    }
+}
+
+#ifndef SLAM_EVEN_D
+#define SLAM_EVEN_D 4
+#endif
+#ifndef SLAM_EVEN_E
+#define SLAM_EVEN_E 7
+#endif
+// workgroups per even block for the D / E roles (T = 5: one output tile per
+// wave; fewer workgroups looping over tiles, 1/2 and 2/3 and 3/4, measured slower)
+constexpr int kBcrEvenD = SLAM_EVEN_D, kBcrEvenE = SLAM_EVEN_E;
+
+template <int T>
+__global__ __launch_bounds__(kBcrThreads) void bcr_even_mfma_kernel(double* __restrict__ D, double* __restrict__ E,
+                                                                    const double* __restrict__ Xs,
+                                                                    const double* __restrict__ Ys,
+                                                                    double* __restrict__ bz, int32_t Wb, int32_t nb,
+                                                                    int32_t s) {
+    constexpr int WB = 16 * T, LD = WB + 1, NTD = T * (T + 1) / 2, NTE = T * T;
+    constexpr int nD = kBcrEvenD, nE = kBcrEvenE;   // workgroups per even block for each role
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* L1 = lds;
+    double* L2 = lds + WB * LD;
+    const int j = 2 * s * blockIdx.x;
+    const int i1 = j - s, i2 = j + s;
+    const bool h1 = i1 >= 0, h2 = i2 < nb, hE = h2 && j + 2 * s < nb;
+    const int y = blockIdx.y;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+    const int64_t B2 = bcr_blk(WB);
+    if (y < nD) {
+        if (!h1 && !h2) return;
+        bcr_stage_pair<T>(h1 ? Ys + i1 * B2 : nullptr, h2 ? Xs + i2 * B2 : nullptr, L1, L2);   // Y1, X2
+        __syncthreads();
+        for (int task = 4 * y + wave; task <= NTD; task += 4 * nD) {   // the staged factors serve several tiles
+        if (task < NTD) {
+            int ti = 0, t = task;
+            while (t > ti) {   // lower tile t -> (ti, tj), tj <= ti
+                t -= ti + 1;
+                ++ti;
+            }
+            const int tj = t;
+            double* Dj = D + j * B2;
+            f64x4 c;   // -(D_j tile): accumulate the products, store the negation
+#pragma unroll
+            for (int g = 0; g < 4; ++g) c[g] = -Dj[(16 * ti + lk + 4 * g) * WB + 16 * tj + lr];
+            if (h1) c = bcr_tile_atb<T>(L1, L1, ti, tj, c);
+            if (h2) c = bcr_tile_atb<T>(L2, L2, ti, tj, c);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Dj[(16 * ti + lk + 4 * g) * WB + 16 * tj + lr] = -c[g];
+        } else if (task == NTD) {
+            const double* z1 = bz + static_cast<int64_t>(h1 ? i1 : 0) * WB;
+            const double* z2 = bz + static_cast<int64_t>(h2 ? i2 : 0) * WB;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const int r = lane + 64 * half;
+                if (r >= WB) continue;
+                double a1 = 0.0, a2 = 0.0;
+#pragma unroll 8
+                for (int k = 0; k < WB; ++k) {
+                    a1 = fma(L1[k * LD + r], h1 ? z1[k] : 0.0, a1);
+                    a2 = fma(L2[k * LD + r], h2 ? z2[k] : 0.0, a2);
+                }
+                bz[static_cast<int64_t>(j) * WB + r] -= a1 + a2;
+            }
+        }
+        }
+    } else {
+        if (!hE) return;
+        bcr_stage_pair<T>(Ys + i2 * B2, Xs + i2 * B2, L1, L2);   // Y2, X2
+        __syncthreads();
+        for (int t = 4 * (y - nD) + wave; t < NTE; t += 4 * nE) {
+            const int ti = t / T, tj = t % T;
+            f64x4 c = {0.0, 0.0, 0.0, 0.0};
+            c = bcr_tile_atb<T>(L1, L2, ti, tj, c);
+            double* Ej = E + j * B2;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Ej[(16 * ti + lk + 4 * g) * WB + 16 * tj + lr] = -c[g];
+        }
+    }
+}
+
+// Last block: the blocked elimination of [D_0 | b_0], then C_0^T x = z by one
+// wave (C_0 in LDS from the elimination).
+template <int T>
+__global__ __launch_bounds__(kBcrThreads) void bcr_top_mfma_kernel(double* __restrict__ D,
+                                                                   const double* __restrict__ bz,
+                                                                   double* __restrict__ x, int32_t Wb,
+                                                                   int32_t* __restrict__ status) {
+    using L = BcrMfmaLds<T>;
+    constexpr int WB = L::WB;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* A = lds;
+    double* Zb = A + WB * L::LDA;
+    double* rdg = Zb + 2 * 16 * L::LDZ;
+    double* y = rdg + WB;
+    bcr_stage_block<T>(D, A);
+    auto rinit = [&](int row, int col) -> double { return col == 0 ? bz[row] : 0.0; };
+    auto out = [&](int row, int col, double v) {
+        if (col == 0) y[row] = v;
+    };
+    const bool bad = bcr_blocked_elim<T>(A, Zb, rdg, 1, rinit, out);
+    if (bad && threadIdx.x == 0) *status = 1;
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        double v0 = tid < WB ? y[tid] : 0.0, v1 = tid + 64 < WB ? y[tid + 64] : 0.0;
+        bcr_backsub_wave(A, L::LDA, rdg, WB, v0, v1);
+        if (tid < WB) x[tid] = v0;
+        if (tid + 64 < WB) x[tid + 64] = v1;
+    }
+}
+
 // ---- host ------------------------------------------------------------------
 
 int bcr_block_rows(int32_t nv, int32_t W) {
@@ -610,15 +1028,64 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim);
         attrs = true;
     }
+    // MFMA path (default) or the register elimination (SLAMHIP_BCR_LEGACY=1, A/B)
+    static const bool legacy = [] {
+        const char* e = getenv("SLAMHIP_BCR_LEGACY");
+        return e && e[0] == '1';
+    }();
+    using OddMFn = void (*)(const double*, const double*, double*, double*, double*, double*, int32_t, int32_t,
+                            int32_t, int32_t*);
+    static const OddMFn odds_m[6] = {bcr_odd_mfma_kernel<1>, bcr_odd_mfma_kernel<2>, bcr_odd_mfma_kernel<3>,
+                                     bcr_odd_mfma_kernel<4>, bcr_odd_mfma_kernel<5>, bcr_odd_mfma_kernel<6>};
+    static const EvenFn evens_m[6] = {bcr_even_mfma_kernel<1>, bcr_even_mfma_kernel<2>, bcr_even_mfma_kernel<3>,
+                                      bcr_even_mfma_kernel<4>, bcr_even_mfma_kernel<5>, bcr_even_mfma_kernel<6>};
+    static const TopFn tops_m[6] = {bcr_top_mfma_kernel<1>, bcr_top_mfma_kernel<2>, bcr_top_mfma_kernel<3>,
+                                    bcr_top_mfma_kernel<4>, bcr_top_mfma_kernel<5>, bcr_top_mfma_kernel<6>};
+    static const size_t lds_m[6] = {BcrMfmaLds<1>::bytes, BcrMfmaLds<2>::bytes, BcrMfmaLds<3>::bytes,
+                                    BcrMfmaLds<4>::bytes, BcrMfmaLds<5>::bytes, BcrMfmaLds<6>::bytes};
+    // the odd blocks' blocked MFMA elimination (SLAMHIP_BCR_ODD_MFMA=1) is kept
+    // for A/B: its single-wave panel factorization is slower than the register
+    // elimination today
+    static const bool odd_mfma = [] {
+        const char* e = getenv("SLAMHIP_BCR_ODD_MFMA");
+        return e && e[0] == '1';
+    }();
+    static bool attrs_m = false;
+    if (!attrs_m) {
+        for (int t = 0; t < 6; ++t) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(odds_m[t]),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_m[t]));
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tops_m[t]),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_m[t]));
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(evens_m[t]),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        }
+        attrs_m = true;
+    }
+    const int T = Wb / 16;
+    // one wave per output tile: D tiles + the rhs wave, then the E' tiles
+    const int even_groups = kBcrEvenD + kBcrEvenE;
     int s = 1;
     for (; s < nb; s *= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);        // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);           // j = 0, 2s, ... < nb
-        hipLaunchKernelGGL(odd, dim3(n_odd, 6), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
-                           stamps);
-        hipLaunchKernelGGL(even, dim3(n_even, 5), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
+        if (legacy) {
+            hipLaunchKernelGGL(odd, dim3(n_odd, 6), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s, status,
+                               stamps);
+            hipLaunchKernelGGL(even, dim3(n_even, 5), dim3(kBcrThreads), lds_even, st, D, E, Xs, Ys, bz, Wb, nb, s);
+        } else {
+            if (odd_mfma)
+                hipLaunchKernelGGL(odds_m[T - 1], dim3(n_odd, 3), dim3(kBcrThreads), lds_m[T - 1], st, D, E, Cs, Xs,
+                                   Ys, bz, Wb, nb, s, status);
+            else
+                hipLaunchKernelGGL(odd, dim3(n_odd, 6), dim3(kBcrThreads), 0, st, D, E, Cs, Xs, Ys, bz, Wb, nb, s,
+                                   status, stamps);
+            hipLaunchKernelGGL(evens_m[T - 1], dim3(n_even, even_groups), dim3(kBcrThreads), lds_even, st, D, E, Xs,
+                               Ys, bz, Wb, nb, s);
+        }
     }
-    hipLaunchKernelGGL(top, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
+    if (legacy) hipLaunchKernelGGL(top, dim3(1), dim3(kBcrThreads), lds_back, st, D, bz, dx, Wb, status);
+    else hipLaunchKernelGGL(tops_m[T - 1], dim3(1), dim3(kBcrThreads), lds_m[T - 1], st, D, bz, dx, Wb, status);
     for (s /= 2; s >= 1; s /= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
         hipLaunchKernelGGL(back, dim3(n_odd), dim3(kBcrThreads), lds_back, st, Cs, Xs, Ys, bz, dx, Wb, nb, s);

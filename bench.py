@@ -76,6 +76,8 @@ def parse():
                    help="phase-1 iterations of the batch scheduler (0 = one launch; -1 = library default)")
     p.add_argument("--sched-heads", type=int, default=-1,
                    help="pairs started on CU-exclusive workgroups in phase 2 (-1 = library default)")
+    p.add_argument("--sched-gangs", default="",
+                   help="G,K: the first G head pairs run as gangs of K workgroups (library default 24,4; 0,2 = off)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
     return p.parse_args()
 
@@ -323,6 +325,9 @@ def main():
         lib.slam_icp_set_schedule(args.sched_probe, 1024)
     if args.sched_heads >= 0:
         lib.slam_icp_set_schedule_heads(args.sched_heads)
+    if args.sched_gangs:
+        g_, k_ = (int(x) for x in args.sched_gangs.split(","))
+        lib.slam_icp_set_schedule_gangs(g_, k_)
     lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)

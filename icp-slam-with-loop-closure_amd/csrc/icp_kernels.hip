@@ -77,7 +77,18 @@ struct IcpArgs {
     int32_t phase_cap;
     int32_t resume;
     float* sched_key;
+    // gangs (GANG kernels only): a pair's query groups dealt over `gang`
+    // workgroups on one XCD that exchange their per-iteration partial sums
+    // through gang_cnt / gang_slots; n_gangs pairs
+    int32_t gang;
+    int32_t n_gangs;
+    uint32_t* gang_cnt;      // [n_gangs * kGangCntStride], zeroed before the launch
+    uint64_t* gang_slots;    // [n_gangs][2][gang][16] partial sums (fp64 bits)
 };
+constexpr int kGangCntStride = 64;    // one 256-B line per gang counter
+constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
+constexpr uint32_t kGangSpinLimit = 1u << 26;   // ~seconds of polling: a lost partner ends the launch
+__device__ int g_gang_timeout;        // set when a gang partner never arrived
 
 // A wave-uniform double moved to SGPRs (v_readfirstlane of both halves).
 __device__ __forceinline__ double uniform_d(double v) {
@@ -299,7 +310,8 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                                                  uint32_t* __restrict__ st, int st_stride,
                                                  float (&M1)[QPT], float (&M2)[QPT], int (&J1)[QPT],
                                                  int& nvisit, bool stamping, unsigned long long (&tsub)[9],
-                                                 bool counting, unsigned long long& nev) {
+                                                 bool counting, unsigned long long& nev,
+                                                 unsigned long long* ghist) {
     const int lane = threadIdx.x & 63;
     unsigned long long t0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
     auto lap = [&](int q) {   // diagnostics: sub-phase s_memtime (workgroup 0, wave 0)
@@ -379,6 +391,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
         if (__ballot(act[k]) == 0) continue;   // wave-uniform
+        int g_live = 0, g_vis = 0;   // diagnostics (stamping): this group's live and visited sub-chunks
         unsigned long long f0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
         auto flap = [&](int q) {   // diagnostics: group-loop sub-phases (workgroup 0, wave 0)
             if (stamping) {
@@ -401,7 +414,10 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             const bool gl = glb <= gM2;
             gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
             uint64_t live = __ballot((sl < nsub) & gl);
-            if (stamping) tsub[3] += __popcll(live);
+            if (stamping) {
+                tsub[3] += __popcll(live);
+                g_live += __popcll(live);
+            }
             flap(6);
             while (live) {
                 // up to kBatch live sub-chunks per batch, straight-line: the box
@@ -436,6 +452,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
                     todo &= todo - 1;
                     const int c8 = (64 * w + static_cast<int>((scpack >> (6 * u)) & 63)) * kSub;
                     ++nvisit;
+                    ++g_vis;
                     if (counting) nev += kSub * __popcll(__ballot((need >> u) & 1u));
                     if ((need >> u) & 1u) {
 #pragma unroll
@@ -453,6 +470,15 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         // lb <= d32 <= (1 + 5u) |q - p|^2, so |q - p| >= sqrt(lb) (1 - 1e-5)
         const float gfar = wave_min_f(gf);
         if (act[k]) st[k * st_stride] = st_pack(sqrtf(fminf(gfar, lmin)) * (1.0f - 1e-5f), ws[k]);
+        const int na = stamping ? __popcll(__ballot(act[k])) : 0;
+        if (stamping && lane == 0) {
+            // diagnostics: per active-lane bucket (1, 2-4, 5-8, 9-16, 17-32, 33-64): group
+            // iterations, live sub-chunks, visited sub-chunks (stamps[96..])
+            const int bk = na <= 1 ? 0 : na <= 4 ? 1 : na <= 8 ? 2 : na <= 16 ? 3 : na <= 32 ? 4 : 5;
+            atomicAdd(ghist + bk, 1ull);
+            atomicAdd(ghist + 8 + bk, static_cast<unsigned long long>(g_live));
+            atomicAdd(ghist + 16 + bk, static_cast<unsigned long long>(g_vis));
+        }
     }
     lap(2);
 }
@@ -471,10 +497,57 @@ __device__ __forceinline__ bool certify(double d1, double s2, double a) {
     return s2 > fc;
 }
 
+// Gang exchange of one iteration's 16 exact partial sums (lane q of every wave
+// holds value q): wave 0 publishes this workgroup's slab with write-through
+// (sc1) stores, drains them and bumps the gang counter (agent scope); every
+// wave polls the counter (sc1 loads) until all `parts` slabs of exchange `e`
+// are in, then sums them in part order (the partials are exact sums on fixed
+// grids, so any order gives the same bits).  Slabs alternate by exchange
+// parity: a part can only reach exchange e + 2 after every part has arrived at
+// e + 1, i.e. after every part has read exchange e.  (MI355X_MICROARCH.md,
+// inter-workgroup visibility: sc1 stores + vmcnt(0) + agent atomic; sc1 poll
+// and sc1 payload loads.)
+__device__ __forceinline__ double gang_exchange(double t, uint32_t* cnt, uint64_t* slots, int part, int parts,
+                                                int e) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    uint64_t* buf = slots + (e & 1) * parts * 16;
+    if (wave == 0) {
+        if (lane < 16)
+            __hip_atomic_store(buf + part * 16 + lane, static_cast<uint64_t>(__double_as_longlong(t)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t target = static_cast<uint32_t>(parts) * static_cast<uint32_t>(e + 1);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kGangSpinLimit) {   // a partner never arrived: flag it, end in finite time
+            if (lane == 0) atomicOr(&g_gang_timeout, 1);
+            break;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double s = 0.0;
+    if (lane < 16) {
+        for (int p = 0; p < parts; ++p)
+            s += __longlong_as_double(static_cast<long long>(
+                __hip_atomic_load(buf + p * 16 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    }
+    return s;
+}
+
 // DIAG: a diagnostics build of the kernel (per-phase s_memtime stamps of
 // workgroup 0, in-kernel candidate-evaluation counter); the product kernels
 // are compiled without any of it.
-template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false, int WPE = 1, bool DIAG = false>
+// GANG: one pair runs on a.gang workgroups (parts); part p holds the query
+// groups (64 consecutive queries) p, p + gang, p + 2 gang, ... and the parts
+// exchange their partial sums every iteration (gang_exchange).  Every part
+// stages pc2 and computes the per-pair constants itself; part 0 writes the
+// outputs.  Results are bit-identical to the one-workgroup kernels.
+template <int BLOCK, int QPT, bool STEP, bool SCREEN, bool PRUNE = false, int WPE = 1, bool DIAG = false,
+          bool GANG = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void icp_kernel(IcpArgs a) {
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -492,11 +565,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     int* qprev = reinterpret_cast<int*>(box8 + cap / kSub);
     uint32_t* qst = reinterpret_cast<uint32_t*>(qprev + BLOCK * QPT);
 
+    // GANG: blocks b and b + 8 share an XCD (round-robin dispatch), so gang g's
+    // parts sit at stride 8: block = ((g / 8) * gang + part) * 8 + g % 8
+    int slot = static_cast<int>(blockIdx.x), part = 0, parts = 1;
+    if constexpr (GANG) {
+        parts = a.gang;
+        const int bx = static_cast<int>(blockIdx.x);
+        slot = (bx / (8 * parts)) * 8 + (bx & 7);
+        part = (bx >> 3) % parts;
+        if (slot >= a.n_gangs) return;   // padding block (uniform)
+    }
     // pair of this workgroup: launch order or the scheduler's order
-    const int b = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
+    const int b = a.order ? a.order[slot] : slot;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+    // query of slot (k, tid): ((k * WAVES + wave) * parts + part) * 64 + lane
+    //   = k * qstride + tid + gshift   (qstride = BLOCK, gshift = 0 without gangs)
+    const int qstride = GANG ? BLOCK * parts : BLOCK;
+    const int gshift = GANG ? (wave * (parts - 1) + part) * 64 : 0;   // wave-uniform
     // resumed phase: out_iters holds -(iterations done) for a paused pair and
     // the final count for a finished one (nothing left to do)
     int it0 = 0;
@@ -517,8 +604,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     // the caller's bounds (max_n1 / max_n2) chose this instance and the LDS
     // size: a pair outside them would be computed wrongly, so it is flagged
     // instead (slam_icp_status returns SLAM_EINVAL) and left undone
-    if (n1 < 1 || n2 < 1 || n1 > BLOCK * QPT || (SCREEN && !resident)) {
-        if (tid == 0) {
+    if (n1 < 1 || n2 < 1 || n1 > qstride * QPT || (SCREEN && !resident)) {
+        if (tid == 0 && part == 0) {
             if (!STEP) a.out_iters[b] = kBadBounds;
             a.out_err[b] = __builtin_nan("");
             atomicOr(&g_icp_status, 1);
@@ -653,7 +740,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     double* hist = (!STEP && a.hist_stride > 0)
                        ? a.out_hist + static_cast<int64_t>(b) * a.hist_stride * 9
                        : nullptr;
-    if (hist && tid == 0 && it0 == 0) store_se2(hist, T);
+    if (hist && tid == 0 && part == 0 && it0 == 0) store_se2(hist, T);
     double last_err = it0 > 0 ? a.out_err[b] : 0.0;
     __syncthreads();
 
@@ -703,7 +790,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 int C1[QPT];
 #pragma unroll
                 for (int k = 0; k < QPT; ++k) {
-                    const int i = k * BLOCK + tid;
+                    const int i = k * qstride + tid + gshift;
                     double x = 0.0, y = 0.0;
                     if (i < n1) {
                         const double2 p = p1[i];
@@ -737,28 +824,28 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         bool vq[QPT];
 #pragma unroll
                         for (int k = 0; k < QPT; ++k) {
-                            const int i = k * BLOCK + tid;
+                            const int i = k * qstride + tid + gshift;
                             const int bp = qprev[k * BLOCK + tid];
                             pred[k] = bp >= 0 ? bp
                                                     : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
                             vq[k] = i < n1;
                         }
                         // groups holding queries (uniform; only the last can be empty)
-                        const int nq = min(QPT, (n1 - 64 * wave + BLOCK - 1) / BLOCK);
+                        const int nq = min(QPT, max(0, (n1 - 64 * wave - gshift + qstride - 1) / qstride));
                         if (QPT > 1 && nq == QPT - 1)
                             nn_window_pruned<QPT, (QPT > 1 ? QPT - 1 : QPT)>(candf, box8, nsub, fx, fy, vq, pred,
                                                                                qst + tid, BLOCK, M1, M2, C1,
                                                                                nscan_total,
-                                                                               stamping, tsub, counting, nev);
+                                                                               stamping, tsub, counting, nev, a.stamps ? a.stamps + 96 : nullptr);
                         else
                             nn_window_pruned<QPT, QPT>(candf, box8, nsub, fx, fy, vq, pred, qst + tid, BLOCK, M1, M2, C1,
-                                                       nscan_total, stamping, tsub, counting, nev);
+                                                       nscan_total, stamping, tsub, counting, nev, a.stamps ? a.stamps + 96 : nullptr);
                     } else {
                         nn_scan_chunked<QPT>(candf, n2_pad, fx, fy, M1, M2, C1);
                         if (counting) {   // full screen + winning-chunk rescan
 #pragma unroll
                             for (int k = 0; k < QPT; ++k)
-                                nev += (n2_pad + kChunk) * __popcll(__ballot(k * BLOCK + tid < n1));
+                                nev += (n2_pad + kChunk) * __popcll(__ballot(k * qstride + tid + gshift < n1));
                         }
                     }
                 }
@@ -773,7 +860,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 }
 #pragma unroll
                 for (int k = 0; k < QPT; ++k) {
-                    const int i = k * BLOCK + tid;
+                    const int i = k * qstride + tid + gshift;
                     double x = 0.0, y = 0.0;
                     if (i < n1) {
                         const double2 p = p1[i];
@@ -846,7 +933,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             stamp(2);
 #pragma unroll
             for (int k = 0; k < QPT; ++k) {
-                const int nb = k * BLOCK + tid < n1 ? bi[k] : -1;
+                const int nb = k * qstride + tid + gshift < n1 ? bi[k] : -1;
                 if constexpr (PRUNE) qprev[k * BLOCK + tid] = nb;
                 else bprev[k] = nb;
             }
@@ -855,7 +942,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             double best[QPT];
 #pragma unroll
             for (int k = 0; k < QPT; ++k) {
-                const int i = k * BLOCK + tid;
+                const int i = k * qstride + tid + gshift;
                 double x = 0.0, y = 0.0;
                 if (i < n1) {
                     const double2 p = p1[i];
@@ -871,7 +958,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 nn_scan_f64<QPT>(cand, n2, 0, qx, qy, best, bi);
                 if (counting) {
 #pragma unroll
-                    for (int k = 0; k < QPT; ++k) nev += static_cast<unsigned long long>(n2) * __popcll(__ballot(k * BLOCK + tid < n1));
+                    for (int k = 0; k < QPT; ++k) nev += static_cast<unsigned long long>(n2) * __popcll(__ballot(k * qstride + tid + gshift < n1));
                 }
             } else {
                 for (int t0 = 0; t0 < n2; t0 += cap) {
@@ -882,7 +969,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     nn_scan_f64<QPT>(cand, cnt, t0, qx, qy, best, bi);
                     if (counting) {
 #pragma unroll
-                        for (int k = 0; k < QPT; ++k) nev += static_cast<unsigned long long>(cnt) * __popcll(__ballot(k * BLOCK + tid < n1));
+                        for (int k = 0; k < QPT; ++k) nev += static_cast<unsigned long long>(cnt) * __popcll(__ballot(k * qstride + tid + gshift < n1));
                     }
                 }
             }
@@ -916,7 +1003,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             for (int q = 0; q < 16; ++q) acc[q] = 0.0;
 #pragma unroll
             for (int k = 0; k < QPT; ++k) {
-                const int i = k * BLOCK + tr;
+                const int i = k * qstride + tr + gshift;
                 if (i < n1) {
                     const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
                     const double2 p = p1[i];
@@ -933,6 +1020,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 }
             }
             tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
+        }
+        if constexpr (GANG) {
+            if (parts > 1)
+                tot = gang_exchange(tot, a.gang_cnt + static_cast<int64_t>(slot) * kGangCntStride,
+                                    a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 16, part, parts, it - it0);
         }
         const double n = static_cast<double>(n1);
         const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
@@ -982,12 +1074,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             int64_t* corr = a.out_corr + a.corr_off[b];
 #pragma unroll
             for (int k = 0; k < QPT; ++k) {
-                const int i = k * BLOCK + tid;
+                const int i = k * qstride + tid + gshift;
                 if (i < n1) corr[i] = bi[k];
             }
             return;
         } else {
-            if (hist && tid == 0) store_se2(hist + 9 * (it + 1), Tn);
+            if (hist && tid == 0 && part == 0) store_se2(hist + 9 * (it + 1), Tn);
             // src/icp.py:86-95 (identical in every thread -> uniform exit)
             const double derr = fabs(last_err - err);
             const bool stop = (err < a.epsilon) || (it > a.max_iters) ||
@@ -1014,7 +1106,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             if (stop) {
                 flush_stamps();
                 if (counting && lane == 0) atomicAdd(a.evals, nev);
-                if (tid == 0) {
+                if (tid == 0 && part == 0) {
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
                     a.out_iters[b] = it + 1;
@@ -1026,7 +1118,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 // last error change orders the survivors for the next phase
                 flush_stamps();
                 if (counting && lane == 0) atomicAdd(a.evals, nev);
-                if (tid == 0) {
+                if (tid == 0 && part == 0) {
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
                     a.out_iters[b] = -(it + 1);
@@ -1084,6 +1176,31 @@ static double shape_efficiency(int block, int qpt) {
     double e = by_qpt[qpt < 16 ? qpt : 16];
     if (block > 384) e *= 0.75;
     return e;
+}
+
+// Gang kernels (pruned screen, batch mode): one query group per wave (QPT 1),
+// BLOCK = 64 x the groups of a pair's largest part.
+struct GangInstance {
+    int block;
+    KernelFn fn;
+};
+static const GangInstance kGangInstances[] = {
+    {64, icp_kernel<64, 1, false, true, true, 1, false, true>},
+    {128, icp_kernel<128, 1, false, true, true, 1, false, true>},
+    {192, icp_kernel<192, 1, false, true, true, 1, false, true>},
+    {256, icp_kernel<256, 1, false, true, true, 1, false, true>},
+    {320, icp_kernel<320, 1, false, true, true, 1, false, true>},
+    {384, icp_kernel<384, 1, false, true, true, 1, false, true>},
+    {512, icp_kernel<512, 1, false, true, true, 1, false, true>},
+};
+
+// the smallest gang instance holding ceil(groups / parts) groups, or NULL
+static const GangInstance* pick_gang_instance(int max_n1, int parts) {
+    const int groups = (max_n1 + 63) / 64;
+    const int per = (groups + parts - 1) / parts;
+    for (const GangInstance& g : kGangInstances)
+        if (g.block >= 64 * per) return &g;
+    return nullptr;
 }
 
 static const Instance* pick_instance(int max_n1, int forced) {
@@ -1160,6 +1277,7 @@ static unsigned long long* g_icp_evals = nullptr;
 // inst_override / lds_min: the scheduler's CU-exclusive head launch (below)
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
                   void* stream, const Instance* inst_override = nullptr, size_t lds_min = 0) {
+    if (B <= 0) return ok();   // e.g. a scheduler tier left empty
     const Instance* inst = inst_override ? inst_override : pick_instance(max_n1, g_forced_instance);
     if (!inst) return fail(SLAM_ETOOBIG, "query scan of %d points exceeds capacity %d", max_n1, kMaxQuery);
     IcpArgs a = args;
@@ -1226,10 +1344,18 @@ static const Instance* pick_head_instance(int max_n1) {
     return best;
 }
 
-// per device: the side stream and the fork / join events (created once, reused)
+// Gangs: the top g_sched_gangs of the head pairs run on g_sched_gang_parts
+// workgroups each (one query group per wave, CU-exclusive, one XCD per gang),
+// which exchange their partial sums every iteration: a lone pair's iteration
+// latency is then one query group's search plus the exchange, not a whole
+// workgroup's.  Results are bit-identical.
+static int g_sched_gangs = 24;
+static int g_sched_gang_parts = 4;
+
+// per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
-    hipStream_t stream = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
 };
 static SideStream* side_stream(int dev) {
     static SideStream side[64];
@@ -1237,13 +1363,44 @@ static SideStream* side_stream(int dev) {
     SideStream& e = side[dev];
     if (!e.stream) {
         if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&e.stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.join2, hipEventDisableTiming) != hipSuccess) {
             e.stream = nullptr;
             return nullptr;
         }
     }
     return &e;
+}
+
+// G pairs (args.order[0..G)) as gangs of `parts` workgroups; cnt (G x
+// kGangCntStride uint32, zeroed on `s` before this) and slots (G x 2 x parts x
+// 16 uint64) are stream-ordered workspace.  Every gang's parts must be
+// co-resident: G * parts workgroups of one CU each stay far below the CU count.
+static int launch_gangs(const IcpArgs& args, int G, int parts, int max_n1, int max_n2, hipStream_t s,
+                        uint32_t* cnt, uint64_t* slots) {
+    const GangInstance* gi = pick_gang_instance(max_n1, parts);
+    if (!gi || parts < 2 || parts > kGangMax || max_n2 > kCandCap) return fail(SLAM_EINVAL, "icp gangs: no instance");
+    IcpArgs a = args;
+    a.stamps = nullptr;
+    a.evals = nullptr;
+    a.cand_cap = ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk;
+    a.gang = parts;
+    a.n_gangs = G;
+    a.gang_cnt = cnt;
+    a.gang_slots = slots;
+    const size_t lds_need = red_doubles(gi->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2) +
+                            static_cast<size_t>(a.cand_cap) * sizeof(float2) +
+                            static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
+                            static_cast<size_t>(gi->block) * 2 * sizeof(int32_t);
+    if (lds_need > kMaxLds) return fail(SLAM_EINVAL, "icp gangs: LDS");
+    const size_t lds = kMaxLds;   // whole CU: a gang's latency is its slowest part
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gi->fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds));
+    const int blocks = (G + 7) / 8 * 8 * parts;
+    hipLaunchKernelGGL(gi->fn, dim3(blocks), dim3(gi->block), lds, s, a);
+    return check_launch("icp gang kernel");
 }
 
 __global__ __launch_bounds__(256) void sched_count_kernel(const int32_t* __restrict__ iters,
@@ -1285,13 +1442,25 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         return launch(false, args, B, max_n1, max_n2, stream);
     hipStream_t s = as_stream(stream);
     const size_t nb = static_cast<size_t>(B);
-    const size_t bytes = (kSchedBuckets + 1) * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float));
+    // tiers of phase 2: gangs (order[0, G)), CU-exclusive heads (order[G, H)),
+    // the rest (order[H, B)) beside them
+    const int heads = g_sched_heads > 0 && B < kHeadsMaxPairs ? min(g_sched_heads, max(B / 16, 1)) : 0;
+    const int parts = g_sched_gang_parts;
+    const bool gang_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap && parts >= 2 &&
+                         pick_gang_instance(max_n1, parts) != nullptr;
+    const int G = gang_ok ? min(g_sched_gangs, heads) : 0;
+    const size_t gang_cnt_bytes = static_cast<size_t>(G) * kGangCntStride * sizeof(uint32_t);
+    const size_t gang_slot_bytes = static_cast<size_t>(G) * 2 * max(parts, 1) * 16 * sizeof(uint64_t);
+    const size_t sched_bytes = ((kSchedBuckets + 1) * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float)) + 255) / 256 * 256;
+    const size_t bytes = sched_bytes + gang_cnt_bytes + gang_slot_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);
     int32_t* bucket = hist + kSchedBuckets + 1;
     int32_t* order = bucket + nb;
     float* key = reinterpret_cast<float*>(order + nb);
+    uint32_t* gang_cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + sched_bytes);
+    uint64_t* gang_slots = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes + gang_cnt_bytes);
     IcpArgs a = args;
     a.phase_cap = probe;
     a.sched_key = key;
@@ -1300,6 +1469,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         const int g = (B + 255) / 256;
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
         (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
+        if (G > 0) (void)hipMemsetAsync(gang_cnt, 0, gang_cnt_bytes, s);
         hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
         hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);
         hipLaunchKernelGGL(sched_scatter_kernel, dim3(g), dim3(256), 0, s, bucket, B, hist, order);
@@ -1309,24 +1479,35 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         a.phase_cap = 0;
         a.resume = 1;
         a.order = order;
-        const int heads = g_sched_heads > 0 && B < kHeadsMaxPairs ? min(g_sched_heads, max(B / 16, 1)) : 0;
-        const Instance* hinst = heads > 0 && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
+        const Instance* hinst = heads > G && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
         int dev = 0;
         SideStream* side = nullptr;
-        if (hinst && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
+        if ((hinst || G > 0) && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
         if (side) {
-            // fork: the head pairs on CU-exclusive workgroups first on the caller's
-            // stream (the GPU is empty after the scheduler kernels: they take the
-            // first CUs), the rest on the side stream behind the fork event, which
-            // resolves after the heads are queued; join before the workspace is freed
-            if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
+            // fork: the gangs and the head pairs on CU-exclusive workgroups first
+            // (the GPU is empty after the scheduler kernels: they take the first
+            // CUs), gangs on the caller's stream, heads on the second side stream,
+            // the rest on the side stream behind the fork event, which resolves
+            // after the first launches are queued; join before the workspace is freed
+            const int H = hinst ? heads : G;
+            if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess ||
+                hipStreamWaitEvent(side->stream2, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
-            if (rc == 0) rc = launch(false, a, heads, max_n1, max_n2, stream, hinst, kMaxLds);
+            if (rc == 0 && G > 0) rc = launch_gangs(a, G, parts, max_n1, max_n2, s, gang_cnt, gang_slots);
+            if (rc == 0 && H > G) {
+                IcpArgs h = a;
+                h.order = order + G;
+                rc = launch(false, h, H - G, max_n1, max_n2, side->stream2, hinst, kMaxLds);
+            }
             IcpArgs t = a;
-            t.order = order + heads;
-            if (rc == 0) rc = launch(false, t, B - heads, max_n1, max_n2, side->stream);
-            if (rc == 0 && hipEventRecord(side->join, side->stream) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: join");
-            if (rc == 0 && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: wait");
+            t.order = order + H;
+            if (rc == 0) rc = launch(false, t, B - H, max_n1, max_n2, side->stream);
+            if (rc == 0 && (hipEventRecord(side->join, side->stream) != hipSuccess ||
+                            hipEventRecord(side->join2, side->stream2) != hipSuccess))
+                rc = fail(SLAM_EHIP, "icp scheduler: join");
+            if (rc == 0 && (hipStreamWaitEvent(s, side->join, 0) != hipSuccess ||
+                            hipStreamWaitEvent(s, side->join2, 0) != hipSuccess))
+                rc = fail(SLAM_EHIP, "icp scheduler: wait");
         } else {
             rc = launch(false, a, B, max_n1, max_n2, stream);
         }
@@ -1376,6 +1557,17 @@ int slam_icp_set_schedule_heads(int heads) {
     g_sched_heads = heads;
     return ok();
 }
+int slam_icp_set_schedule_gangs(int gangs, int parts) {
+    if (gangs < 0 || parts < 2 || parts > kGangMax) return fail(SLAM_EINVAL, "schedule: gangs %d parts %d", gangs, parts);
+    g_sched_gangs = gangs;
+    g_sched_gang_parts = parts;
+    return ok();
+}
+int slam_icp_gang_timeouts(void) {
+    int v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_gang_timeout), sizeof(int)) != hipSuccess) return fail(SLAM_EHIP, "gang timeouts: read");
+    return v;
+}
 int slam_icp_set_schedule(int probe_iters, int min_pairs) {
     if (probe_iters < 0 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: negative argument");
     g_sched_probe = probe_iters;
@@ -1388,9 +1580,15 @@ int slam_icp_set_schedule(int probe_iters, int min_pairs) {
 // out_err NaN), then clears the flag.
 int slam_icp_status(void* stream) {
     if (hipStreamSynchronize(as_stream(stream)) != hipSuccess) return fail(SLAM_EHIP, "icp status: stream sync");
-    int st = 0;
-    if (hipMemcpyFromSymbol(&st, HIP_SYMBOL(g_icp_status), sizeof(int)) != hipSuccess)
+    int st = 0, gt = 0;
+    if (hipMemcpyFromSymbol(&st, HIP_SYMBOL(g_icp_status), sizeof(int)) != hipSuccess ||
+        hipMemcpyFromSymbol(&gt, HIP_SYMBOL(g_gang_timeout), sizeof(int)) != hipSuccess)
         return fail(SLAM_EHIP, "icp status: read");
+    if (gt != 0) {
+        const int zero = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gang_timeout), &zero, sizeof(int));
+        return fail(SLAM_EHIP, "icp: a gang's workgroups were not co-resident (partner timeout); results invalid");
+    }
     if (st == 0) return ok();
     const int zero = 0;
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_icp_status), &zero, sizeof(int));

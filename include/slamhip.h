@@ -202,16 +202,27 @@ int slam_icp_set_screen(int mode);
  * every pair runs probe_iters iterations, then the unfinished ones resume in
  * order of their last error change (slowest-converging first), so the long
  * tail of iteration counts does not start late.  probe_iters = 0: one launch.
- * Defaults (4, 1024).  Results are identical either way (with heads = 0). */
+ * Defaults (4, 1024).  Results are identical either way. */
 int slam_icp_set_schedule(int probe_iters, int min_pairs);
 /* Phase 2 of the scheduler starts the (at most) `heads` pairs the probe keyed
  * slowest (one per 16 pairs at most) first, on CU-exclusive 512-thread
  * workgroups; the rest runs beside them on a library-owned second stream,
  * joined back before the call's work ends: the strong-scaling tail.  Batches
- * below 8,192 pairs only (a full C3 batch keeps every CU for the bulk).  Their
- * sums run over another wave layout, so their results equal the single launch
- * to rounding (iterations equal).  0 = off; default 64. */
+ * below 8,192 pairs only (a full C3 batch keeps every CU for the bulk).  Sums
+ * are order-free (exact on fixed grids), so results are bit-identical to the
+ * single launch.  0 = off; default 64. */
 int slam_icp_set_schedule_heads(int heads);
+/* The first `gangs` of those head pairs run as gangs of `parts` workgroups
+ * (2..17) each: a pair's 64-query groups are dealt over the parts, which sit on
+ * one XCD, hold one CU each, and exchange their exact partial sums every
+ * iteration through a stream-ordered workspace (agent-scope write-through
+ * stores and counter).  Results are bit-identical to the one-workgroup
+ * kernels.  gangs = 0: off; defaults (24, 4). */
+int slam_icp_set_schedule_gangs(int gangs, int parts);
+/* Nonzero if a gang's workgroups ever failed to meet (a partner not resident
+ * for ~seconds; the launch then ended without valid results).  slam_icp_status
+ * reports and clears it as SLAM_EHIP. */
+int slam_icp_gang_timeouts(void);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver: 0 auto (block cyclic reduction when the band allows it),
  * 1 band Cholesky, 2 block cyclic reduction (falls back to 1 if not allowed). */
@@ -219,8 +230,9 @@ int slam_gn_set_solver(int mode);
 /* Block rows of the cyclic-reduction solver for (nv, W), 0 = not applicable. */
 int slam_gn_bcr_block_rows(int32_t nv, int32_t W);
 /* Diagnostics: per-phase s_memtime totals of workgroup 0 into a device buffer of
- * >= 144 uint64 (wave 0's sub-phases in [0, 16), every wave's phase totals in
- * [16 + 8 * wave, 24 + 8 * wave)); NULL turns stamping off. */
+ * >= 160 uint64 (wave 0's sub-phases in [0, 16), every wave's phase totals in
+ * [16 + 8 * wave, 24 + 8 * wave), the pruned search's group iterations, live and
+ * visited sub-chunks by active-lane bucket in [96, 120)); NULL turns stamping off. */
 int slam_icp_set_stamps(void* dev_buf);
 /* Count candidate-distance evaluations performed (all lanes) into a device
  * uint64 (atomic add per wave); NULL turns counting off.  Stamps and the

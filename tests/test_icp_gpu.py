@@ -385,6 +385,44 @@ def test_default_schedule_large_batch(k):
     assert np.array_equal(phased.tf, single.tf) and np.array_equal(phased.err, single.err)
 
 
+def test_gangs_are_bit_identical(k):
+    """Gangs (a pair's 64-query groups dealt over 2..17 workgroups that
+    exchange their exact partial sums every iteration) return the single
+    launch's transforms, errors, iteration counts and histories bit for bit:
+    every part count, every pair a gang (64 of 64 heads), and the default
+    tiers (8 gangs beside 56 CU-exclusive heads)."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 1100
+    seq, inits = _sequence_pairs(n, seed=2025)
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    try:
+        assert lib.slam_icp_set_schedule(0, 1024) == 0
+        single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+        assert lib.slam_icp_set_schedule(4, 1024) == 0
+        runs = {}
+        for gangs, parts in ((8, 4), (64, 2), (64, 3), (64, 5), (64, 9), (64, 17), (1, 4)):
+            assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
+            runs[(gangs, parts)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+            assert lib.slam_icp_gang_timeouts() == 0
+        assert lib.slam_icp_set_schedule_gangs(64, 4) == 0   # rotation-only, max_iters stop inside phase 2
+        ro = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=7, rotation_only=True)
+        assert lib.slam_icp_set_schedule(0, 1024) == 0
+        ro_single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=7, rotation_only=True)
+        assert lib.slam_icp_set_schedule_gangs(1, 1) != 0   # a gang needs two parts
+    finally:
+        lib.slam_icp_set_schedule(4, 1024)
+        lib.slam_icp_set_schedule_gangs(24, 4)
+    assert single.iters.max() > 30
+    for key, r in runs.items():
+        assert np.array_equal(r.iters, single.iters), key
+        assert np.array_equal(r.tf, single.tf) and np.array_equal(r.err, single.err), key
+        for h0, h1 in zip(single.hist, r.hist):
+            assert np.array_equal(h0, h1), key
+    assert np.array_equal(ro.iters, ro_single.iters)
+    assert np.array_equal(ro.tf, ro_single.tf) and np.array_equal(ro.err, ro_single.err)
+
+
 def test_default_schedule_c3_shape_vs_oracle(k, oracle):
     """The benchmarked path itself: 2,400 consecutive pairs of 1081-point scans
     (the C3 stream generator, seed 2025) through the DEFAULT two-phase

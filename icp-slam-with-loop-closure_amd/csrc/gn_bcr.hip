@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "gn_bcr.hpp"
 
 namespace slamhip {
 
@@ -974,7 +975,7 @@ int bcr_block_rows(int32_t nv, int32_t W) {
 int64_t bcr_work_size(int32_t nv, int32_t W) {
     const int Wb = ((max(W, 1) + 15) / 16) * 16;
     const int64_t nb = (nv + Wb - 1) / Wb;
-    return 5 * nb * bcr_blk(Wb) + 2 * nb * Wb;
+    return max(5 * nb * bcr_blk(Wb) + 2 * nb * Wb, bcr_gj_work_size(nv, Wb));
 }
 
 // Solve H dx = rhs (H in band storage, work of bcr_work_size doubles); *dx_out
@@ -983,6 +984,38 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
               double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps) {
     const int nb = (nv + Wb - 1) / Wb;
     const int64_t B2 = bcr_blk(Wb);
+    // default: the explicit-inverse levels (gn_bcr_gj.hip); the Cholesky paths
+    // below stay selectable for A/B (SLAMHIP_BCR_CHOL=1, SLAMHIP_BCR_LEGACY=1)
+    static const bool chol = [] {
+        const char* e = getenv("SLAMHIP_BCR_CHOL");
+        const char* l = getenv("SLAMHIP_BCR_LEGACY");
+        return (e && e[0] == '1') || (l && l[0] == '1');
+    }();
+    if (!chol) {
+        const BcrGjBufs g = bcr_gj_bufs(work, nv, Wb);
+        const int64_t tot = nb * B2;
+        hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs,
+                           nv, W, Wb, nb, g.D, g.E0, g.bz);
+        int rc = bcr_gj_levels(g, nv, Wb, status, st);
+        if (rc != 0) return rc;
+        using TopFn = void (*)(double*, const double*, double*, int32_t, int32_t*);
+        static const TopFn tops[6] = {bcr_top_mfma_kernel<1>, bcr_top_mfma_kernel<2>, bcr_top_mfma_kernel<3>,
+                                      bcr_top_mfma_kernel<4>, bcr_top_mfma_kernel<5>, bcr_top_mfma_kernel<6>};
+        static const size_t lds_t[6] = {BcrMfmaLds<1>::bytes, BcrMfmaLds<2>::bytes, BcrMfmaLds<3>::bytes,
+                                        BcrMfmaLds<4>::bytes, BcrMfmaLds<5>::bytes, BcrMfmaLds<6>::bytes};
+        static bool attrs_t = false;
+        if (!attrs_t) {
+            for (int t = 0; t < 6; ++t)
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tops[t]),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_t[t]));
+            attrs_t = true;
+        }
+        hipLaunchKernelGGL(tops[Wb / 16 - 1], dim3(1), dim3(kBcrThreads), lds_t[Wb / 16 - 1], st, g.D, g.bz, g.x, Wb,
+                           status);
+        rc = bcr_gj_back(g, nv, Wb, st);
+        *dx_out = g.x;
+        return rc;
+    }
     double* D = work;
     double* E = D + nb * B2;
     double* Xs = E + nb * B2;

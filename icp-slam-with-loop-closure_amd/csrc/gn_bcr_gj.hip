@@ -1,0 +1,566 @@
+// gn_bcr_gj.hip — block cyclic reduction of the Gauss-Newton normal equations
+// on explicit block inverses (gfx950 / MI355X; the default BCR path).
+//
+// The band of H cut into blocks of Wb rows is block tridiagonal (gn_bcr.hip:
+// D_i = H[i,i], E_i = H[i+1,i]).  Level s eliminates the odd blocks
+// i = s, 3s, ... in parallel.  Where gn_bcr.hip factors D_i = C C^T and carries
+// C^-1 through triangular solves (80 barrier-separated pivots per level on the
+// dependent chain), this path inverts D_i outright — blocked Gauss-Jordan with
+// 16-column steps: one wave inverts the 16 x 16 diagonal tile, the row, trailing
+// and column tiles are MFMA products (v_mfma_f64_16x16x4_f64), 3 barriers per
+// step, 3 T barriers per block — and every product that follows is a GEMM:
+//   G = D_i^-1,  X_i = G A[i,p],  Y_i = G A[i,n],  z_i = G b_i
+//   Sp_i = A[p,i] X_i   (-> D_p),   Sn_i = A[n,i] Y_i   (-> D_n)
+//   E'_p = -A[n,i] X_i  (the new coupling p <-> n, next level's E)
+// with A[i,p] = E_p, A[n,i] = E_i (block rows of H).  A small combine kernel
+// then forms D_j -= Sn_{j-s} + Sp_{j+s}, b_j -= A[j,i] z_i for the even blocks
+// (fixed order: deterministic), and the back-substitution is two mat-vecs,
+// x_i = z_i - X_i x_p - Y_i x_n.  Block 0 is solved last by gn_bcr.hip's top
+// kernel.  Each odd block runs on 2T workgroups (blockIdx.y): X side column
+// tile q < T, Y side column tile q - T; every one inverts D_i itself (the
+// inversion is the chain, the redundancy costs CU time only).  Gauss-Jordan
+// without pivoting is stable for the SPD blocks here; results agree with the
+// Cholesky paths to rounding (tests: 1e-8 against oracle/gn_oracle.py).
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+#include "gn_bcr.hpp"
+
+namespace slamhip {
+
+namespace bcrgj {
+
+constexpr int kThreads = 256;
+#ifdef SLAM_GJ_STAMPS
+// tools/gj_ubench.hip: s_memtime per phase, thread 0 of workgroup (0, 0)
+__device__ unsigned long long g_gj_stamps[8];
+#define GJ_T0() unsigned long long t0_ = __builtin_amdgcn_s_memtime()
+#define GJ_STAMP(q)                                                                            \
+    do {                                                                                       \
+        const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                          \
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_gj_stamps[q] += t1_ - t0_; \
+        t0_ = t1_;                                                                             \
+    } while (0)
+#else
+#define GJ_T0() (void)0
+#define GJ_STAMP(q) (void)0
+#endif
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f64_16x16x4_f64: lane l holds A[l & 15][l >> 4] and B[l >> 4][l & 15];
+// C/D element g of lane l is (row (l >> 4) + 4 g, col l & 15)
+// (cdna_hip_programming.md, fragment layout: f64).
+__device__ __forceinline__ f64x4 mma(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int T>
+struct Lds {
+    static constexpr int WB = 16 * T;
+    static constexpr int LDA = WB + 1;   // block / its inverse: [WB][LDA] (odd stride spreads banks)
+    static constexpr int LDC = 17;       // one column tile: [WB][LDC]
+    static constexpr size_t doubles = static_cast<size_t>(WB) * LDA + static_cast<size_t>(WB) * LDC + 2 * WB;
+    static constexpr size_t bytes = doubles * sizeof(double);
+};
+
+// D_i (WB x WB, global, row-major) -> A (LDS): every load in flight at once.
+template <int T>
+__device__ __forceinline__ void stage(const double* __restrict__ src, double* A) {
+    constexpr int WB = 16 * T, LDA = WB + 1, PER = T * T;   // (16T)^2 / 256
+    double g[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) g[q] = src[threadIdx.x + kThreads * q];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + kThreads * q;
+        A[(e / WB) * LDA + e % WB] = g[q];
+    }
+}
+
+// Lane `src`'s double in every lane (src may differ per lane): ds_bpermute.
+__device__ __forceinline__ double bperm_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src * 4, static_cast<int>(b & 0xffffffff));
+    const int hi = __builtin_amdgcn_ds_bpermute(src * 4, static_cast<int>(b >> 32));
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+// Element kq (0..3, a constant after unrolling) of each quad, in every lane of the quad (DPP).
+__device__ __forceinline__ double quad_bcast(double v, int kq) {
+    const long long b = __double_as_longlong(v);
+    int lo = static_cast<int>(b & 0xffffffff), hi = static_cast<int>(b >> 32);
+    switch (kq) {
+        case 0: lo = __builtin_amdgcn_update_dpp(0, lo, 0x00, 0xF, 0xF, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x00, 0xF, 0xF, false); break;
+        case 1: lo = __builtin_amdgcn_update_dpp(0, lo, 0x55, 0xF, 0xF, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x55, 0xF, 0xF, false); break;
+        case 2: lo = __builtin_amdgcn_update_dpp(0, lo, 0xAA, 0xF, 0xF, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0xAA, 0xF, 0xF, false); break;
+        default: lo = __builtin_amdgcn_update_dpp(0, lo, 0xFF, 0xF, 0xF, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0xFF, 0xF, 0xF, false); break;
+    }
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+// The 16 x 16 tile at P (row stride LDA) -> its inverse, by ONE wave: a
+// register Gauss-Jordan (lane l: row r = l >> 2, columns c0..c0+3, c0 = 4 (l & 3));
+// per pivot the row-k values come by ds_bpermute from lane 4k + (l & 3), a[r][k]
+// by a DPP quad broadcast, the pivot by v_readlane: no LDS round trip and no
+// barrier on the chain.  Returns "a pivot was not positive".
+template <int LDA>
+__device__ __forceinline__ bool tile_inv16(double* P, int lane) {
+    const int r = lane >> 2, cq = lane & 3, c0 = 4 * cq;
+    bool bad = false;
+    double v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = P[r * LDA + c0 + q];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int kq = k >> 2, kr = k & 3;
+        const double ark = quad_bcast(v[kr], kq);
+        const double akk = readlane_d(v[kr], 4 * k + kq);
+        double akc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) akc[q] = bperm_d(v[q], 4 * k + cq);
+        bad |= !(akk > 0.0);
+        // reciprocal pivot: v_rcp_f64 and two Newton steps (a few ulp; no fp64
+        // division sequence on the chain)
+        double pv = __builtin_amdgcn_rcp(akk);
+        pv = fma(pv, fma(-akk, pv, 1.0), pv);
+        pv = fma(pv, fma(-akk, pv, 1.0), pv);
+        const double m = ark * pv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = c0 + q;
+            double nv = fma(-m, akc[q], v[q]);
+            if (c == k) nv = -m;
+            if (r == k) nv = c == k ? pv : akc[q] * pv;
+            v[q] = nv;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) P[r * LDA + c0 + q] = v[q];
+    return bad;
+}
+
+// In-place inverse of the SPD block in A by blocked Gauss-Jordan.  Step kb:
+//   R  (MFMA)    row tiles A[kb,j] <- Pinv A[kb,j]; column tiles A[i,kb] -> C
+//   U  (MFMA)    A[i,j] -= C_i A[kb,j] (i, j != kb);  A[i,kb] = -C_i Pinv
+// with look-ahead: in U, wave 0 updates the next diagonal tile first and
+// inverts it (tile_inv16) while waves 1-3 update every other tile, so the
+// pivot chain of step kb + 1 runs beside step kb's trailing update.  Two
+// barriers per step.  C: [WB][17] LDS scratch.  Returns "a pivot was not
+// positive" (wave 0).
+template <int T>
+__device__ bool gj_invert(double* A, double* C) {
+    constexpr int WB = 16 * T, LDA = WB + 1, LDC = 17;
+    constexpr int NTU = T * (T - 1);                         // U tiles: rows != kb
+    constexpr int NPW = NTU > 0 ? (NTU + 2) / 3 : 1;         // per wave of waves 1-3
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lk = lane >> 4;
+    bool bad = false;
+    GJ_T0();
+    if (wave == 0) bad |= tile_inv16<LDA>(A, lane);
+    __syncthreads();
+    GJ_STAMP(0);
+    for (int kb = 0; kb < T; ++kb) {
+        double* P = A + 16 * kb * LDA + 16 * kb;
+        // R: row tiles (one per wave), the old column tiles to C
+        for (int t = wave; t < T; t += 4) {
+            if (t == kb) continue;
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+            double a[4], b[4];
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+                a[k4] = P[lr * LDA + 4 * k4 + lk];
+                b[k4] = A[(16 * kb + 4 * k4 + lk) * LDA + 16 * t + lr];
+            }
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) acc = mma(a[k4], b[k4], acc);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) A[(16 * kb + lk + 4 * g) * LDA + 16 * t + lr] = acc[g];
+        }
+#pragma unroll
+        for (int q = 0; q < WB * 16 / kThreads; ++q) {
+            const int e = tid + kThreads * q, rr = e >> 4, cc = e & 15;
+            C[rr * LDC + cc] = A[rr * LDA + 16 * kb + cc];
+        }
+        __syncthreads();
+        GJ_STAMP(1);
+        const int nx = kb + 1;   // the next diagonal tile (if nx < T)
+        // one U tile (ti, tj): A[ti,tj] -= C_ti A[kb,tj]  (tj == kb: A[ti,kb] = -C_ti Pinv)
+        auto load_tile = [&](int ti, int tj, f64x4& acc, double (&a)[4], double (&b)[4]) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = tj == kb ? 0.0 : A[(16 * ti + lk + 4 * g) * LDA + 16 * tj + lr];
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+                a[k4] = -C[(16 * ti + lr) * LDC + 4 * k4 + lk];
+                b[k4] = A[(16 * kb + 4 * k4 + lk) * LDA + 16 * tj + lr];
+            }
+        };
+        if (wave == 0) {
+            if (nx < T) {
+                f64x4 acc;
+                double a[4], b[4];
+                load_tile(nx, nx, acc, a, b);
+#pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4) acc = mma(a[k4], b[k4], acc);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) A[(16 * nx + lk + 4 * g) * LDA + 16 * nx + lr] = acc[g];
+                bad |= tile_inv16<LDA>(A + 16 * nx * LDA + 16 * nx, lane);   // this wave's writes precede its reads
+            }
+        } else {
+            // waves 1-3: tiles t = (wave - 1) + 3 u, in chunks of 4 with their
+            // operands loaded first and the MFMA chains interleaved
+#pragma unroll
+            for (int u0 = 0; u0 < NPW; u0 += 4) {
+                constexpr int CH = 4;
+                f64x4 acc[CH];
+                double a[CH][4], b[CH][4];
+                int off[CH];
+#pragma unroll
+                for (int c = 0; c < CH; ++c) {
+                    const int t = (wave - 1) + 3 * (u0 + c);
+                    const int tt = t < NTU ? t : 0;
+                    const int ti0 = tt / T, tj = tt % T;
+                    const int ti = ti0 + (ti0 >= kb ? 1 : 0);
+                    const bool ok = u0 + c < NPW && t < NTU && !(ti == nx && tj == nx);
+                    off[c] = ok ? (16 * ti + lk) * LDA + 16 * tj + lr : -1;
+                    load_tile(ti, tj, acc[c], a[c], b[c]);
+                }
+#pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+                    for (int c = 0; c < CH; ++c) acc[c] = mma(a[c][k4], b[c][k4], acc[c]);
+#pragma unroll
+                for (int c = 0; c < CH; ++c)
+                    if (off[c] >= 0) {
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) A[off[c] + 4 * g * LDA] = acc[c][g];
+                    }
+            }
+        }
+        __syncthreads();
+        GJ_STAMP(2);
+    }
+    return bad;
+}
+
+// Odd blocks of level s: grid (n_odd, 2 ng + 1) with ng = ceil(T / cpw)
+// column-tile groups of cpw tiles (the host picks cpw so the level's
+// workgroups fit the chip at once).  Every workgroup inverts D_i itself, then:
+//   q < ng        X side, column tiles of group q:  X_i = G E_p (-> Xs_i, LDS),
+//                 Sp_i = E_p^T X_i (-> SP_i), E'_p = -E_i X_i (-> En_p);
+//   ng <= q < 2ng Y side: Y_i = G E_i^T (-> Ys_i), Sn_i = E_i Y_i (-> SN_i);
+//   q = 2 ng      z_i = G b_i (-> bz_i), E_p^T z_i (-> SPb_i), E_i z_i (-> SNb_i).
+template <int T>
+__global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict__ D, const double* __restrict__ Ec,
+                                                      double* __restrict__ En, double* __restrict__ Xs,
+                                                      double* __restrict__ Ys, double* __restrict__ SP,
+                                                      double* __restrict__ SN, double* __restrict__ bz,
+                                                      double* __restrict__ SPb, double* __restrict__ SNb, int32_t nb,
+                                                      int32_t s, int32_t cpw, int32_t* __restrict__ status) {
+    using L = Lds<T>;
+    constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, K4 = WB / 4;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* A = lds;
+    double* C = A + WB * LDA;
+    double* vz = C + WB * LDC;   // [2][WB]: b_i, z_i
+    const int ng = (T + cpw - 1) / cpw;
+    const int q = blockIdx.y;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const bool hn = n < nb;
+    const bool zwg = q == 2 * ng;
+    const bool xside = q < ng;
+    if (!xside && !zwg && !hn) return;   // the last block has no right neighbour
+    const int g0 = (xside ? q : q - ng) * cpw;
+    const int tj0 = zwg ? 0 : g0, tj1 = zwg ? 0 : min(T, g0 + cpw);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB;
+    const double* Ep = Ec + p * B2;   // A[i, p]
+    const double* Ei = Ec + i * B2;   // A[n, i]
+    GJ_T0();
+    stage<T>(D + i * B2, A);
+    if (zwg && tid < WB) vz[tid] = bz[static_cast<int64_t>(i) * WB + tid];
+    __syncthreads();
+    GJ_STAMP(3);
+    const bool bad = gj_invert<T>(A, C);   // A = G (ends with a barrier)
+    GJ_STAMP(4);
+    if (bad && q == 0 && tid == 0) *status = 1;
+    for (int tj = tj0; tj < tj1; ++tj) {
+        // first product: column tile tj of X_i = G E_p or Y_i = G E_i^T: the
+        // tile of E (the B operand, shared by every output tile) is loaded once,
+        // all K4 fragments in flight; a wave's output tiles run interleaved
+        double* Out1 = (xside ? Xs : Ys) + i * B2;
+        {
+            constexpr int N1 = (T + 3) / 4;
+            double bf[K4];
+#pragma unroll
+            for (int k4 = 0; k4 < K4; ++k4)
+                bf[k4] = xside ? Ep[(4 * k4 + lk) * WB + 16 * tj + lr] : Ei[(16 * tj + lr) * WB + 4 * k4 + lk];
+            f64x4 acc[N1];
+#pragma unroll
+            for (int u = 0; u < N1; ++u) acc[u] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k4 = 0; k4 < K4; ++k4)
+#pragma unroll
+                for (int u = 0; u < N1; ++u) {
+                    const int ti = min(wave + 4 * u, T - 1);
+                    acc[u] = mma(A[(16 * ti + lr) * LDA + 4 * k4 + lk], bf[k4], acc[u]);
+                }
+#pragma unroll
+            for (int u = 0; u < N1; ++u) {
+                const int ti = wave + 4 * u;
+                if (ti < T) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int row = 16 * ti + lk + 4 * g;
+                        Out1[row * WB + 16 * tj + lr] = acc[u][g];
+                        C[row * LDC + lr] = acc[u][g];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        GJ_STAMP(5);
+        // second products on that column tile (in C, the B operand):
+        // Sp = E_p^T X, E' = -E_i X  |  Sn = E_i Y; each task's K4 A fragments
+        // in flight at once
+        {
+            const int ntask = xside ? (hn ? 2 * T : T) : T;
+            constexpr int N2 = (2 * T + 3) / 4;
+            double bf[K4];
+#pragma unroll
+            for (int k4 = 0; k4 < K4; ++k4) bf[k4] = C[(4 * k4 + lk) * LDC + lr];
+#pragma unroll
+            for (int u = 0; u < N2; ++u) {
+                const int t = wave + 4 * u;
+                if (t < ntask) {   // wave-uniform
+                    const int ti = t % T;
+                    const bool e = t >= T;
+                    double af[K4];
+#pragma unroll
+                    for (int k4 = 0; k4 < K4; ++k4)
+                        af[k4] = (xside && !e) ? Ep[(4 * k4 + lk) * WB + 16 * ti + lr] : Ei[(16 * ti + lr) * WB + 4 * k4 + lk];
+                    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int k4 = 0; k4 < K4; ++k4) acc = mma(af[k4], bf[k4], acc);
+                    double* Out2 = xside ? (e ? En + p * B2 : SP + i * B2) : SN + i * B2;
+                    const double sg = e ? -1.0 : 1.0;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Out2[(16 * ti + lk + 4 * g) * WB + 16 * tj + lr] = sg * acc[g];
+                }
+            }
+        }
+        __syncthreads();   // C is rewritten by the next column tile
+        GJ_STAMP(6);
+    }
+    if (zwg) {
+        // three mat-vecs, each over the whole workgroup: rows r = lane, lane + 64
+        // of wave w sum k in [w WB/4, (w+1) WB/4), the quarters meet in LDS (C)
+        constexpr int KQ = WB / 4;
+        double* red = C;   // [4][WB]
+        const int k0 = wave * KQ;
+        auto quarters = [&](auto term) {   // red[wave][r] = sum_k term(r, k) over the wave's quarter
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int r = lane + 64 * h;
+                if (r < WB) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int k = 0; k < KQ; ++k) acc += term(r, k0 + k);
+                    red[wave * WB + r] = acc;
+                }
+            }
+            __syncthreads();
+        };
+        quarters([&](int r, int k) { return A[r * LDA + k] * vz[k]; });   // z = G b
+        if (tid < WB) {
+            const double z = ((red[tid] + red[WB + tid]) + red[2 * WB + tid]) + red[3 * WB + tid];
+            vz[WB + tid] = z;
+            bz[static_cast<int64_t>(i) * WB + tid] = z;
+        }
+        __syncthreads();
+        quarters([&](int r, int k) { return Ep[k * WB + r] * vz[WB + k]; });   // E_p^T z
+        if (tid < WB)
+            SPb[static_cast<int64_t>(i) * WB + tid] = ((red[tid] + red[WB + tid]) + red[2 * WB + tid]) + red[3 * WB + tid];
+        __syncthreads();
+        if (hn) {
+            quarters([&](int r, int k) { return Ei[r * WB + k] * vz[WB + k]; });   // E_i z
+            if (tid < WB)
+                SNb[static_cast<int64_t>(i) * WB + tid] =
+                    ((red[tid] + red[WB + tid]) + red[2 * WB + tid]) + red[3 * WB + tid];
+        }
+    }
+}
+
+// Even blocks of level s (j = 0, 2s, ...): D_j -= Sn_{j-s} + Sp_{j+s} and
+// b_j -= SNb_{j-s} + SPb_{j+s}, in that order.  grid (n_even, kCombineSplit).
+constexpr int kCombineSplit = 4;
+__global__ __launch_bounds__(kThreads) void combine_kernel(double* __restrict__ D, const double* __restrict__ SP,
+                                                          const double* __restrict__ SN, double* __restrict__ bz,
+                                                          const double* __restrict__ SPb,
+                                                          const double* __restrict__ SNb, int32_t WB, int32_t nb,
+                                                          int32_t s) {
+    const int j = 2 * s * blockIdx.x;
+    const int i1 = j - s, i2 = j + s;
+    const bool h1 = i1 >= 0, h2 = i2 < nb;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB;
+    double* Dj = D + j * B2;
+    for (int64_t e = blockIdx.y * kThreads + threadIdx.x; e < B2; e += kCombineSplit * kThreads) {
+        double v = Dj[e];
+        if (h1) v -= SN[i1 * B2 + e];
+        if (h2) v -= SP[i2 * B2 + e];
+        Dj[e] = v;
+    }
+    if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < WB) {
+        const int r = threadIdx.x;
+        double v = bz[static_cast<int64_t>(j) * WB + r];
+        if (h1) v -= SNb[static_cast<int64_t>(i1) * WB + r];
+        if (h2) v -= SPb[static_cast<int64_t>(i2) * WB + r];
+        bz[static_cast<int64_t>(j) * WB + r] = v;
+    }
+}
+
+// A double moved between lanes of a 16-lane row by DPP (both halves).
+template <int CTRL>
+__device__ __forceinline__ double dpp_row(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+// Back-substitution of the odd blocks of level s: x_i = z_i - X_i x_p - Y_i x_n
+// (16 x 16 threads: thread (tr, tc) sums columns tc + 16 w of rows tr + 16 u from
+// 128 B row segments; DPP row sums).
+template <int T>
+__global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict__ Xs, const double* __restrict__ Ys,
+                                                       const double* __restrict__ bz, double* __restrict__ x,
+                                                       int32_t nb, int32_t s) {
+    constexpr int WB = 16 * T;
+    __shared__ double xpn[2 * WB];
+    const int tid = threadIdx.x;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const bool hn = n < nb;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB;
+    for (int k = tid; k < WB; k += kThreads) {
+        xpn[k] = x[static_cast<int64_t>(p) * WB + k];
+        xpn[WB + k] = hn ? x[static_cast<int64_t>(n) * WB + k] : 0.0;
+    }
+    __syncthreads();
+    const int tr = tid >> 4, tc = tid & 15;
+    const double* X = Xs + i * B2;
+    const double* Y = Ys + i * B2;
+    double v[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const int r = tr + 16 * u;
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            const int k = tc + 16 * w;
+            a0 = fma(X[r * WB + k], xpn[k], a0);
+            if (hn) a1 = fma(Y[r * WB + k], xpn[WB + k], a1);
+        }
+        v[u] = a0 + a1;
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        v[u] += dpp_row<0xB1>(v[u]);    // quad_perm [1,0,3,2]
+        v[u] += dpp_row<0x4E>(v[u]);    // quad_perm [2,3,0,1]
+        v[u] += dpp_row<0x124>(v[u]);   // row_ror 4
+        v[u] += dpp_row<0x128>(v[u]);   // row_ror 8
+    }
+    if (tc == 0) {
+#pragma unroll
+        for (int u = 0; u < T; ++u) {
+            const int r = tr + 16 * u;
+            x[static_cast<int64_t>(i) * WB + r] = bz[static_cast<int64_t>(i) * WB + r] - v[u];
+        }
+    }
+}
+
+}  // namespace bcrgj
+
+constexpr int kBcrGjSlots = 2 * 256;   // odd-kernel workgroups resident at once (2 per CU)
+
+BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb) {
+    const int64_t nb = (nv + Wb - 1) / Wb;
+    const int64_t B2 = static_cast<int64_t>(Wb) * Wb;
+    BcrGjBufs b;
+    b.D = work;
+    b.E0 = b.D + nb * B2;
+    b.E1 = b.E0 + nb * B2;
+    b.Xs = b.E1 + nb * B2;
+    b.Ys = b.Xs + nb * B2;
+    b.SP = b.Ys + nb * B2;
+    b.SN = b.SP + nb * B2;
+    b.bz = b.SN + nb * B2;
+    b.SPb = b.bz + nb * Wb;
+    b.SNb = b.SPb + nb * Wb;
+    b.x = b.SNb + nb * Wb;
+    return b;
+}
+
+int64_t bcr_gj_work_size(int32_t nv, int32_t Wb) {
+    const int64_t nb = (nv + Wb - 1) / Wb;
+    return 7 * nb * Wb * Wb + 4 * nb * Wb;
+}
+
+// The levels of the explicit-inverse reduction, after bcr_load_kernel filled
+// D, E0 and bz; block 0 is left for the caller's top kernel (D, bz).
+int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, hipStream_t st) {
+    const int nb = (nv + Wb - 1) / Wb;
+    using OddFn = void (*)(const double*, const double*, double*, double*, double*, double*, double*, double*,
+                           double*, double*, int32_t, int32_t, int32_t, int32_t*);
+    static const OddFn odds[6] = {bcrgj::odd_kernel<1>, bcrgj::odd_kernel<2>, bcrgj::odd_kernel<3>,
+                                  bcrgj::odd_kernel<4>, bcrgj::odd_kernel<5>, bcrgj::odd_kernel<6>};
+    static const size_t lds[6] = {bcrgj::Lds<1>::bytes, bcrgj::Lds<2>::bytes, bcrgj::Lds<3>::bytes,
+                                  bcrgj::Lds<4>::bytes, bcrgj::Lds<5>::bytes, bcrgj::Lds<6>::bytes};
+    static bool attrs = false;
+    if (!attrs) {   // not a stream operation: the launch sequence stays graph-capturable
+        for (int t = 0; t < 6; ++t)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(odds[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(lds[t]));
+        attrs = true;
+    }
+    const int T = Wb / 16;
+    int lv = 0;
+    for (int s = 1; s < nb; s *= 2, ++lv) {
+        const int n_odd = (nb - s + 2 * s - 1) / (2 * s);   // i = s, 3s, ... < nb
+        const int n_even = (nb + 2 * s - 1) / (2 * s);      // j = 0, 2s, ... < nb
+        double* Ec = (lv & 1) ? b.E1 : b.E0;
+        double* En = (lv & 1) ? b.E0 : b.E1;
+        // column tiles per workgroup: the fewest that keep the level's
+        // workgroups within two per CU (64 KB of LDS each) -> one wave of them
+        int cpw = 1;
+        while (cpw < T && n_odd * (2 * ((T + cpw - 1) / cpw) + 1) > kBcrGjSlots) ++cpw;
+        const int ng = (T + cpw - 1) / cpw;
+        hipLaunchKernelGGL(odds[T - 1], dim3(n_odd, 2 * ng + 1), dim3(bcrgj::kThreads), lds[T - 1], st, b.D, Ec, En,
+                           b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb, b.SNb, nb, s, cpw, status);
+        hipLaunchKernelGGL(bcrgj::combine_kernel, dim3(n_even, bcrgj::kCombineSplit), dim3(bcrgj::kThreads), 0, st,
+                           b.D, b.SP, b.SN, b.bz, b.SPb, b.SNb, Wb, nb, s);
+    }
+    return check_launch("gn bcr (explicit inverse) kernels");
+}
+
+// Back-substitution, level by level in reverse, after the top kernel wrote x_0.
+int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, hipStream_t st) {
+    const int nb = (nv + Wb - 1) / Wb;
+    using BackFn = void (*)(const double*, const double*, const double*, double*, int32_t, int32_t);
+    static const BackFn backs[6] = {bcrgj::back_kernel<1>, bcrgj::back_kernel<2>, bcrgj::back_kernel<3>,
+                                    bcrgj::back_kernel<4>, bcrgj::back_kernel<5>, bcrgj::back_kernel<6>};
+    int s = 1;
+    while (s < nb) s *= 2;
+    for (s /= 2; s >= 1; s /= 2) {
+        const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
+        hipLaunchKernelGGL(backs[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bz, b.x, nb, s);
+    }
+    return check_launch("gn bcr (explicit inverse) back-substitution");
+}
+
+}  // namespace slamhip

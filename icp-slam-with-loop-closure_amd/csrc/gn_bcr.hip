@@ -996,22 +996,8 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         const int64_t tot = nb * B2;
         hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs,
                            nv, W, Wb, nb, g.D, g.E0, g.bz);
-        int rc = bcr_gj_levels(g, nv, Wb, status, st);
+        int rc = bcr_gj_levels(g, nv, Wb, status, st);   // levels + block 0
         if (rc != 0) return rc;
-        using TopFn = void (*)(double*, const double*, double*, int32_t, int32_t*);
-        static const TopFn tops[6] = {bcr_top_mfma_kernel<1>, bcr_top_mfma_kernel<2>, bcr_top_mfma_kernel<3>,
-                                      bcr_top_mfma_kernel<4>, bcr_top_mfma_kernel<5>, bcr_top_mfma_kernel<6>};
-        static const size_t lds_t[6] = {BcrMfmaLds<1>::bytes, BcrMfmaLds<2>::bytes, BcrMfmaLds<3>::bytes,
-                                        BcrMfmaLds<4>::bytes, BcrMfmaLds<5>::bytes, BcrMfmaLds<6>::bytes};
-        static bool attrs_t = false;
-        if (!attrs_t) {
-            for (int t = 0; t < 6; ++t)
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tops[t]),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_t[t]));
-            attrs_t = true;
-        }
-        hipLaunchKernelGGL(tops[Wb / 16 - 1], dim3(1), dim3(kBcrThreads), lds_t[Wb / 16 - 1], st, g.D, g.bz, g.x, Wb,
-                           status);
         rc = bcr_gj_back(g, nv, Wb, st);
         *dx_out = g.x;
         return rc;

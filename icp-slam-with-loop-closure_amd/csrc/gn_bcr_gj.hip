@@ -12,12 +12,13 @@
 //   G = D_i^-1,  X_i = G A[i,p],  Y_i = G A[i,n],  z_i = G b_i
 //   Sp_i = A[p,i] X_i   (-> D_p),   Sn_i = A[n,i] Y_i   (-> D_n)
 //   E'_p = -A[n,i] X_i  (the new coupling p <-> n, next level's E)
-// with A[i,p] = E_p, A[n,i] = E_i (block rows of H).  A small combine kernel
-// then forms D_j -= Sn_{j-s} + Sp_{j+s}, b_j -= A[j,i] z_i for the even blocks
-// (fixed order: deterministic), and the back-substitution is two mat-vecs,
-// x_i = z_i - X_i x_p - Y_i x_n.  Block 0 is solved last by gn_bcr.hip's top
-// kernel.  Each odd block runs on 2T workgroups (blockIdx.y): X side column
-// tile q < T, Y side column tile q - T; every one inverts D_i itself (the
+// with A[i,p] = E_p, A[n,i] = E_i (block rows of H).  The even blocks' updates
+// D_j -= Sn_{j-s} + Sp_{j+s}, b_j -= A[j,i] z_i are applied lazily, in level
+// order (deterministic), by the kernel that next reads D_j: the odd kernel of
+// the level at which j is odd, or the block-0 combine; the back-substitution
+// is two mat-vecs,
+// x_i = z_i - X_i x_p - Y_i x_n.  Block 0 is solved last (top_kernel).  Each odd block runs on 2 ng + 1 workgroups (blockIdx.y): X side and
+// Y side column-tile groups and one for z; every one inverts D_i itself (the
 // inversion is the chain, the redundancy costs CU time only).  Gauss-Jordan
 // without pivoting is stable for the SPD blocks here; results agree with the
 // Cholesky paths to rounding (tests: 1e-8 against oracle/gn_oracle.py).
@@ -34,6 +35,7 @@ namespace slamhip {
 namespace bcrgj {
 
 constexpr int kThreads = 256;
+constexpr int kCombineSplit = 4;   // workgroups per block of a combine
 #ifdef SLAM_GJ_STAMPS
 // tools/gj_ubench.hip: s_memtime per phase, thread 0 of workgroup (0, 0)
 __device__ unsigned long long g_gj_stamps[8];
@@ -126,15 +128,15 @@ __device__ __forceinline__ bool tile_inv16(double* P, int lane) {
         double pv = __builtin_amdgcn_rcp(akk);
         pv = fma(pv, fma(-akk, pv, 1.0), pv);
         pv = fma(pv, fma(-akk, pv, 1.0), pv);
-        const double m = ark * pv;
+        // one rank-1 update for every entry: with column k's pivot entry taken
+        // as a_kk - 1 and row k's as a_kk + 1, a - u v^T / a_kk gives row k / a_kk,
+        // -column k / a_kk and 1 / a_kk at the pivot (2 selects per pivot instead
+        // of 8; relative rounding ~a_kk eps on row k)
+        const double u = r == k ? akk - 1.0 : ark;
+        akc[kr] = cq == kq ? akk + 1.0 : akc[kr];
+        const double m = u * pv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int c = c0 + q;
-            double nv = fma(-m, akc[q], v[q]);
-            if (c == k) nv = -m;
-            if (r == k) nv = c == k ? pv : akc[q] * pv;
-            v[q] = nv;
-        }
+        for (int q = 0; q < 4; ++q) v[q] = fma(-m, akc[q], v[q]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) P[r * LDA + c0 + q] = v[q];
@@ -150,7 +152,7 @@ __device__ __forceinline__ bool tile_inv16(double* P, int lane) {
 // barriers per step.  C: [WB][17] LDS scratch.  Returns "a pivot was not
 // positive" (wave 0).
 template <int T>
-__device__ bool gj_invert(double* A, double* C) {
+__device__ __forceinline__ bool gj_invert(double* A, double* C) {
     constexpr int WB = 16 * T, LDA = WB + 1, LDC = 17;
     constexpr int NTU = T * (T - 1);                         // U tiles: rows != kb
     constexpr int NPW = NTU > 0 ? (NTU + 2) / 3 : 1;         // per wave of waves 1-3
@@ -245,20 +247,22 @@ __device__ bool gj_invert(double* A, double* C) {
     return bad;
 }
 
-// Odd blocks of level s: grid (n_odd, 2 ng + 1) with ng = ceil(T / cpw)
-// column-tile groups of cpw tiles (the host picks cpw so the level's
-// workgroups fit the chip at once).  Every workgroup inverts D_i itself, then:
-//   q < ng        X side, column tiles of group q:  X_i = G E_p (-> Xs_i, LDS),
-//                 Sp_i = E_p^T X_i (-> SP_i), E'_p = -E_i X_i (-> En_p);
-//   ng <= q < 2ng Y side: Y_i = G E_i^T (-> Ys_i), Sn_i = E_i Y_i (-> SN_i);
-//   q = 2 ng      z_i = G b_i (-> bz_i), E_p^T z_i (-> SPb_i), E_i z_i (-> SNb_i).
+// Odd blocks of level s: grid (n_odd [+ combine workgroups], 2 ng + 1) with
+// ng = ceil(T / cpw) column-tile groups of cpw tiles (the host picks cpw per
+// level so its workgroups fit the chip).  Every workgroup inverts D_i itself,
+// then, per column tile of its group:
+//   q < ng   X_i = G E_p (-> Xs_i, LDS), Sp_i = E_p^T X_i (-> SP_i),
+//            E'_p = -E_i X_i (-> En_p);
+//   q < 2ng  Y_i = G E_i^T (-> Ys_i), Sn_i = E_i Y_i (-> SN_i);
+//   q = 2ng  z_i = G b_i (-> bz_i), E_p^T z_i (-> SPb_i), E_i z_i (-> SNb_i).
 template <int T>
-__global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict__ D, const double* __restrict__ Ec,
+__global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D, const double* __restrict__ Ec,
                                                       double* __restrict__ En, double* __restrict__ Xs,
                                                       double* __restrict__ Ys, double* __restrict__ SP,
                                                       double* __restrict__ SN, double* __restrict__ bz,
                                                       double* __restrict__ SPb, double* __restrict__ SNb, int32_t nb,
-                                                      int32_t s, int32_t cpw, int32_t* __restrict__ status) {
+                                                      int32_t s, int32_t cpw, int32_t n_odd,
+                                                      int32_t* __restrict__ status) {
     using L = Lds<T>;
     constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, K4 = WB / 4;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -267,23 +271,90 @@ __global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict_
     double* vz = C + WB * LDC;   // [2][WB]: b_i, z_i
     const int ng = (T + cpw - 1) / cpw;
     const int q = blockIdx.y;
+    const int sp = s / 2;   // the previous level (0: none)
+    const int tid = threadIdx.x;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB;
+    if (static_cast<int>(blockIdx.x) >= n_odd) {
+        // combine workgroups: block j = 2s x' stays even at this level and takes
+        // the previous level's updates D_j -= Sn_{j-sp} + Sp_{j+sp} (b_j likewise)
+        const int j = 2 * s * (blockIdx.x - n_odd);
+        if (j >= nb || q >= kCombineSplit || sp == 0) return;
+        const bool h1 = j - sp >= 0, h2 = j + sp < nb;
+        double* Dj = D + j * B2;
+        for (int64_t e = q * kThreads + tid; e < B2; e += kCombineSplit * kThreads) {
+            double v = Dj[e];
+            if (h1) v -= SN[(j - sp) * B2 + e];
+            if (h2) v -= SP[(j + sp) * B2 + e];
+            Dj[e] = v;
+        }
+        if (q == 0 && tid < WB) {
+            double v = bz[static_cast<int64_t>(j) * WB + tid];
+            if (h1) v -= SNb[static_cast<int64_t>(j - sp) * WB + tid];
+            if (h2) v -= SPb[static_cast<int64_t>(j + sp) * WB + tid];
+            bz[static_cast<int64_t>(j) * WB + tid] = v;
+        }
+        return;
+    }
+    if (q > 2 * ng) return;   // grid.y padded for the combine workgroups
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
     const bool hn = n < nb;
-    const bool zwg = q == 2 * ng;
-    const bool xside = q < ng;
-    if (!xside && !zwg && !hn) return;   // the last block has no right neighbour
-    const int g0 = (xside ? q : q - ng) * cpw;
+    // side 0: X / Sp / E', 2: Y / Sn, 3: z
+    const int side = q == 2 * ng ? 3 : (q < ng ? 0 : 2);
+    const bool zwg = side == 3;
+    const bool xside = side == 0;
+    if (side == 2 && !hn) return;   // the last block has no right neighbour
+    const int g0 = (q % ng) * cpw;
     const int tj0 = zwg ? 0 : g0, tj1 = zwg ? 0 : min(T, g0 + cpw);
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 15, lk = lane >> 4;
-    const int64_t B2 = static_cast<int64_t>(WB) * WB;
     const double* Ep = Ec + p * B2;   // A[i, p]
     const double* Ei = Ec + i * B2;   // A[n, i]
     GJ_T0();
-    stage<T>(D + i * B2, A);
-    if (zwg && tid < WB) vz[tid] = bz[static_cast<int64_t>(i) * WB + tid];
+    // D_i and b_i with the previous level's Schur updates folded in while
+    // staging: D_i -= Sn_{i-sp} + Sp_{i+sp} (older levels reached D_i through
+    // the combine workgroups of their next level: every block is at most one
+    // level behind, and the subtraction order is the per-level sequence)
+    {
+        constexpr int PER = T * T;
+        const double* Di = D + i * B2;
+        const double* sn = SN + (i - sp) * B2;
+        const double* spp = SP + (i + sp) * B2;
+        const bool h1 = sp > 0, h2 = sp > 0 && i + sp < nb;
+        // three passes (D_i, then - Sn, then - Sp), each with its loads in flight
+        // together: at most 2 x PER doubles live (the kernel's register budget)
+        double g[PER];
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) g[qq] = Di[tid + kThreads * qq];
+        if (h1) {
+            double a1[PER];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) a1[qq] = sn[tid + kThreads * qq];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) g[qq] -= a1[qq];
+        }
+        if (h2) {
+            double a2[PER];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) a2[qq] = spp[tid + kThreads * qq];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) g[qq] -= a2[qq];
+        }
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) {
+            const int e = tid + kThreads * qq;
+            A[(e / WB) * LDA + e % WB] = g[qq];
+        }
+    }
+    if (zwg && tid < WB) {
+        double v = bz[static_cast<int64_t>(i) * WB + tid];
+        if (sp > 0) {
+            v -= SNb[static_cast<int64_t>(i - sp) * WB + tid];
+            if (i + sp < nb) v -= SPb[static_cast<int64_t>(i + sp) * WB + tid];
+        }
+        vz[tid] = v;
+    }
     __syncthreads();
     GJ_STAMP(3);
     const bool bad = gj_invert<T>(A, C);   // A = G (ends with a barrier)
@@ -329,8 +400,8 @@ __global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict_
         // Sp = E_p^T X, E' = -E_i X  |  Sn = E_i Y; each task's K4 A fragments
         // in flight at once
         {
-            const int ntask = xside ? (hn ? 2 * T : T) : T;
             constexpr int N2 = (2 * T + 3) / 4;
+            const int ntask = (xside && hn) ? 2 * T : T;
             double bf[K4];
 #pragma unroll
             for (int k4 = 0; k4 < K4; ++k4) bf[k4] = C[(4 * k4 + lk) * LDC + lr];
@@ -339,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict_
                 const int t = wave + 4 * u;
                 if (t < ntask) {   // wave-uniform
                     const int ti = t % T;
-                    const bool e = t >= T;
+                    const bool e = t >= T;   // X side: the new coupling
                     double af[K4];
 #pragma unroll
                     for (int k4 = 0; k4 < K4; ++k4)
@@ -347,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict_
                     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                     for (int k4 = 0; k4 < K4; ++k4) acc = mma(af[k4], bf[k4], acc);
-                    double* Out2 = xside ? (e ? En + p * B2 : SP + i * B2) : SN + i * B2;
+                    double* Out2 = e ? En + p * B2 : xside ? SP + i * B2 : SN + i * B2;
                     const double sg = e ? -1.0 : 1.0;
 #pragma unroll
                     for (int g = 0; g < 4; ++g) Out2[(16 * ti + lk + 4 * g) * WB + 16 * tj + lr] = sg * acc[g];
@@ -369,7 +440,7 @@ __global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict_
                 const int r = lane + 64 * h;
                 if (r < WB) {
                     double acc = 0.0;
-#pragma unroll
+#pragma unroll 5
                     for (int k = 0; k < KQ; ++k) acc += term(r, k0 + k);
                     red[wave * WB + r] = acc;
                 }
@@ -396,32 +467,53 @@ __global__ __launch_bounds__(kThreads) void odd_kernel(const double* __restrict_
     }
 }
 
-// Even blocks of level s (j = 0, 2s, ...): D_j -= Sn_{j-s} + Sp_{j+s} and
-// b_j -= SNb_{j-s} + SPb_{j+s}, in that order.  grid (n_even, kCombineSplit).
-constexpr int kCombineSplit = 4;
-__global__ __launch_bounds__(kThreads) void combine_kernel(double* __restrict__ D, const double* __restrict__ SP,
-                                                          const double* __restrict__ SN, double* __restrict__ bz,
-                                                          const double* __restrict__ SPb,
-                                                          const double* __restrict__ SNb, int32_t WB, int32_t nb,
-                                                          int32_t s) {
-    const int j = 2 * s * blockIdx.x;
-    const int i1 = j - s, i2 = j + s;
-    const bool h1 = i1 >= 0, h2 = i2 < nb;
+// Block 0 after the last level sl: D_0 -= Sp_sl, b_0 -= SPb_sl (its earlier
+// levels came through the combine workgroups) while staging, the same
+// Gauss-Jordan inversion, then x_0 = G b_0 (one workgroup).
+template <int T>
+__global__ __launch_bounds__(kThreads) void top_kernel(const double* __restrict__ D, const double* __restrict__ SP,
+                                                      const double* __restrict__ bz, const double* __restrict__ SPb,
+                                                      double* __restrict__ x, int32_t sl, int32_t* __restrict__ status) {
+    using L = Lds<T>;
+    constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, PER = T * T, KQ = WB / 4;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* A = lds;
+    double* C = A + WB * LDA;
+    double* vz = C + WB * LDC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t B2 = static_cast<int64_t>(WB) * WB;
-    double* Dj = D + j * B2;
-    for (int64_t e = blockIdx.y * kThreads + threadIdx.x; e < B2; e += kCombineSplit * kThreads) {
-        double v = Dj[e];
-        if (h1) v -= SN[i1 * B2 + e];
-        if (h2) v -= SP[i2 * B2 + e];
-        Dj[e] = v;
+    {
+        double g[PER], a1[PER];
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) {
+            g[qq] = D[tid + kThreads * qq];
+            a1[qq] = sl > 0 ? SP[sl * B2 + tid + kThreads * qq] : 0.0;
+        }
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) {
+            const int e = tid + kThreads * qq;
+            A[(e / WB) * LDA + e % WB] = sl > 0 ? g[qq] - a1[qq] : g[qq];
+        }
     }
-    if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < WB) {
-        const int r = threadIdx.x;
-        double v = bz[static_cast<int64_t>(j) * WB + r];
-        if (h1) v -= SNb[static_cast<int64_t>(i1) * WB + r];
-        if (h2) v -= SPb[static_cast<int64_t>(i2) * WB + r];
-        bz[static_cast<int64_t>(j) * WB + r] = v;
+    if (tid < WB) vz[tid] = sl > 0 ? bz[tid] - SPb[static_cast<int64_t>(sl) * WB + tid] : bz[tid];
+    __syncthreads();
+    const bool bad = gj_invert<T>(A, C);
+    if (bad && tid == 0) *status = 1;
+    double* red = C;   // [4][WB]: the quarters of x = G b
+    const int k0 = wave * KQ;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int r = lane + 64 * h;
+        if (r < WB) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < KQ; ++k) acc += A[r * LDA + k0 + k] * vz[k0 + k];
+            red[wave * WB + r] = acc;
+        }
     }
+    __syncthreads();
+    if (tid < WB) x[tid] = ((red[tid] + red[WB + tid]) + red[2 * WB + tid]) + red[3 * WB + tid];
 }
 
 // A double moved between lanes of a 16-lane row by DPP (both halves).
@@ -455,16 +547,24 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
     const int tr = tid >> 4, tc = tid & 15;
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
+    // every X / Y load in flight before the first FMA
+    double xv[T][T], yv[T][T];
+#pragma unroll
+    for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            xv[u][w] = X[(tr + 16 * u) * WB + tc + 16 * w];
+            yv[u][w] = hn ? Y[(tr + 16 * u) * WB + tc + 16 * w] : 0.0;
+        }
     double v[T];
 #pragma unroll
     for (int u = 0; u < T; ++u) {
-        const int r = tr + 16 * u;
         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
         for (int w = 0; w < T; ++w) {
             const int k = tc + 16 * w;
-            a0 = fma(X[r * WB + k], xpn[k], a0);
-            if (hn) a1 = fma(Y[r * WB + k], xpn[WB + k], a1);
+            a0 = fma(xv[u][w], xpn[k], a0);
+            a1 = fma(yv[u][w], xpn[WB + k], a1);
         }
         v[u] = a0 + a1;
     }
@@ -512,11 +612,11 @@ int64_t bcr_gj_work_size(int32_t nv, int32_t Wb) {
 }
 
 // The levels of the explicit-inverse reduction, after bcr_load_kernel filled
-// D, E0 and bz; block 0 is left for the caller's top kernel (D, bz).
+// D, E0 and bz, and the block-0 solve (x_0 in b.x).
 int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, hipStream_t st) {
     const int nb = (nv + Wb - 1) / Wb;
-    using OddFn = void (*)(const double*, const double*, double*, double*, double*, double*, double*, double*,
-                           double*, double*, int32_t, int32_t, int32_t, int32_t*);
+    using OddFn = void (*)(double*, const double*, double*, double*, double*, double*, double*, double*,
+                           double*, double*, int32_t, int32_t, int32_t, int32_t, int32_t*);
     static const OddFn odds[6] = {bcrgj::odd_kernel<1>, bcrgj::odd_kernel<2>, bcrgj::odd_kernel<3>,
                                   bcrgj::odd_kernel<4>, bcrgj::odd_kernel<5>, bcrgj::odd_kernel<6>};
     static const size_t lds[6] = {bcrgj::Lds<1>::bytes, bcrgj::Lds<2>::bytes, bcrgj::Lds<3>::bytes,
@@ -529,22 +629,48 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, h
         attrs = true;
     }
     const int T = Wb / 16;
-    int lv = 0;
+    int lv = 0, last = 1;
     for (int s = 1; s < nb; s *= 2, ++lv) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);   // i = s, 3s, ... < nb
         const int n_even = (nb + 2 * s - 1) / (2 * s);      // j = 0, 2s, ... < nb
         double* Ec = (lv & 1) ? b.E1 : b.E0;
         double* En = (lv & 1) ? b.E0 : b.E1;
-        // column tiles per workgroup: the fewest that keep the level's
-        // workgroups within two per CU (64 KB of LDS each) -> one wave of them
-        int cpw = 1;
-        while (cpw < T && n_odd * (2 * ((T + cpw - 1) / cpw) + 1) > kBcrGjSlots) ++cpw;
+        // column tiles per workgroup (cpw), by a cost model of the measured phases
+        // (inversion ~42k cycles, X / Y product ~6k, Sp + E' ~11k per column
+        // tile) over the rounds of kBcrGjSlots resident workgroups.  (A third
+        // workgroup set for E' beside Sp measured slower: 2,530 -> 2,395 it/s.)
+        int cpw = T;
+        double best = 1e30;
+        for (int c = 1; c <= T; ++c) {
+            const int wgs = n_odd * (2 * ((T + c - 1) / c) + 1);
+            const int rounds = (wgs + kBcrGjSlots - 1) / kBcrGjSlots;
+            const double est = rounds * (42.0 + c * 17.0);
+            if (est < best) {
+                best = est;
+                cpw = c;
+            }
+        }
         const int ng = (T + cpw - 1) / cpw;
-        hipLaunchKernelGGL(odds[T - 1], dim3(n_odd, 2 * ng + 1), dim3(bcrgj::kThreads), lds[T - 1], st, b.D, Ec, En,
-                           b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb, b.SNb, nb, s, cpw, status);
-        hipLaunchKernelGGL(bcrgj::combine_kernel, dim3(n_even, bcrgj::kCombineSplit), dim3(bcrgj::kThreads), 0, st,
-                           b.D, b.SP, b.SN, b.bz, b.SPb, b.SNb, Wb, nb, s);
+        // + the combine workgroups of the blocks that stay even (j = 0, 2s, ...)
+        const int n_comb = s > 1 ? n_even : 0;
+        hipLaunchKernelGGL(odds[T - 1], dim3(n_odd + n_comb, max(2 * ng + 1, bcrgj::kCombineSplit)),
+                           dim3(bcrgj::kThreads), lds[T - 1], st, b.D, Ec, En, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb,
+                           b.SNb, nb, s, cpw, n_odd, status);
+        last = s;
     }
+    // block 0 (always even): the last level's Sp, then x_0
+    using TopFn = void (*)(const double*, const double*, const double*, const double*, double*, int32_t, int32_t*);
+    static const TopFn tops[6] = {bcrgj::top_kernel<1>, bcrgj::top_kernel<2>, bcrgj::top_kernel<3>,
+                                  bcrgj::top_kernel<4>, bcrgj::top_kernel<5>, bcrgj::top_kernel<6>};
+    static bool attrs_t = false;
+    if (!attrs_t) {
+        for (int t = 0; t < 6; ++t)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tops[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(lds[t]));
+        attrs_t = true;
+    }
+    hipLaunchKernelGGL(tops[T - 1], dim3(1), dim3(bcrgj::kThreads), lds[T - 1], st, b.D, b.SP, b.bz, b.SPb, b.x,
+                       nb > 1 ? last : 0, status);
     return check_launch("gn bcr (explicit inverse) kernels");
 }
 

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../icp-slam-with-loop-closure_amd/csrc"
 OUT=../../ab/$1
 mkdir -p $OUT
 objs=""
-for f in icp_kernels pgo_kernels gn_kernels gn_bcr grid_kernels; do
+for f in icp_kernels pgo_kernels gn_kernels gn_bcr gn_bcr_gj grid_kernels; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
       -I../../include $2 -c $f.hip -o $OUT/$f.o &
   objs="$objs $OUT/$f.o"

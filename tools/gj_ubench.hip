@@ -66,7 +66,7 @@ int main() {
             while (cpw < T && n_odd * (2 * ((T + cpw - 1) / cpw) + 1) > 512) ++cpw;
             const int ng = (T + cpw - 1) / cpw;
             hipLaunchKernelGGL(bcrgj::odd_kernel<T>, dim3(n_odd, 2 * ng + 1), dim3(bcrgj::kThreads), bcrgj::Lds<T>::bytes,
-                               0, b.D, b.E0, b.E1, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb, b.SNb, nb, 1, cpw, st);
+                               0, b.D, b.E0, b.E1, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb, b.SNb, nb, 1, cpw, n_odd, st);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;

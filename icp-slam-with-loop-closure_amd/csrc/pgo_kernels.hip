@@ -208,6 +208,10 @@ __global__ void sgd_weights_kernel(int32_t N, const int32_t* __restrict__ A, con
 }
 
 constexpr int kRelaxBlock = 512;
+#ifndef SLAM_RELAX_THREADS
+#define SLAM_RELAX_THREADS 256
+#endif
+constexpr int kRelaxThreads = SLAM_RELAX_THREADS;   // the relaxation workgroup: one wave per SIMD (512: 14.9 ms/step at C4, 256: 13.1, 128: 13.0)
 
 // Inclusive prefix sums of 1/M per column: C[0] = 0, C[i+1] = C[i] + invM[i].
 // One workgroup, chunked block scan (fixed order).  The relaxation then reads
@@ -321,7 +325,7 @@ constexpr int kLdsPoses = 6144;
 constexpr int kMaxOffBlocks = 2048;
 
 template <bool IN_LDS>
-__global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
+__global__ __launch_bounds__(kRelaxThreads) void sgd_relax_kernel(
     double* __restrict__ g_poses, int32_t N, const int32_t* __restrict__ A, const int32_t* __restrict__ B,
     const double* __restrict__ TF, const int32_t* __restrict__ Kp, const double* __restrict__ C,
     const double* __restrict__ gamma, double lr, double sigma, int32_t sh) {
@@ -336,12 +340,12 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
     const int bs = 1 << sh;
     if (tid == 0) rd_count = 0;
 
-    for (int i = tid; i < 3 * nblk; i += kRelaxBlock) {
+    for (int i = tid; i < 3 * nblk; i += kRelaxThreads) {
         off[i] = 0.0;
         cA[i] = 0.0;
     }
     if (IN_LDS) {
-        for (int i = tid; i < 3 * N; i += kRelaxBlock) P[i] = g_poses[i];
+        for (int i = tid; i < 3 * N; i += kRelaxThreads) P[i] = g_poses[i];
     }
     __syncthreads();
 
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
         if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if ((tid & 63) == 0) __hip_atomic_fetch_add(&rd_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t rd_target = static_cast<uint32_t>(kRelaxBlock / 64) * static_cast<uint32_t>(k + 1);
+        const uint32_t rd_target = static_cast<uint32_t>(kRelaxThreads / 64) * static_cast<uint32_t>(k + 1);
         // ---- explicit nodes (a's block remainder, b's block) ----------------------
         {
             int i = cur.ni;
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
 #pragma unroll
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
                 }
-                t += kRelaxBlock;   // more than one explicit node per thread only when 2^(sh+1) > block
+                t += kRelaxThreads;   // more than one explicit node per thread only when 2^(sh+1) > block
                 if (t >= 2 * bs) break;
                 const int n1 = min(N, (ba + 1) << sh) - (a + 1);
                 const int n2 = bb > ba ? min(N, (bb + 1) << sh) - (bb << sh) : 0;
@@ -461,7 +465,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
             }
         }
         // ---- whole blocks: ramp (ba, bb) as C coefficients, tail (bb, nblk) --------
-        for (int q = ba + 1 + tid; q < nblk; q += kRelaxBlock) {
+        for (int q = ba + 1 + tid; q < nblk; q += kRelaxThreads) {
             if (q < bb) {
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_relax_kernel(
         cur = nxt;
     }
     // fold the lazy terms back
-    for (int i = tid; i < N; i += kRelaxBlock) {
+    for (int i = tid; i < N; i += kRelaxThreads) {
         const int q = i >> sh;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -563,13 +567,13 @@ int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int
         const size_t lds = offb + 3 * static_cast<size_t>(N) * sizeof(double);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxBlock), lds, s, poses, N, A, Bv, TF,
+        hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxThreads), lds, s, poses, N, A, Bv, TF,
                            Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
     } else {
         // off + cA reach 2 x 3 x 2048 doubles (96 KiB): above the 64 KiB default
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(offb));
-        hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxBlock), offb, s, poses, N, A, Bv,
+        hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxThreads), offb, s, poses, N, A, Bv,
                            TF, Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
     }
     return check_launch("pgo sgd kernels");

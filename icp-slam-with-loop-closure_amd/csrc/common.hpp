@@ -169,6 +169,10 @@ __device__ __forceinline__ RsumGrid rsum_grid(double bound, int n) {
 }
 
 __device__ __forceinline__ void rsum_add(double x, const RsumGrid& g, double& s1, double& s2) {
+#ifdef SLAM_ABL_SUMS
+    s1 += x;   // ablation build (timing only): plain sums
+    return;
+#endif
     const double h1 = (x + g.m1) - g.m1;
     const double r = x - h1;
     const double h2 = (r + g.m2) - g.m2;

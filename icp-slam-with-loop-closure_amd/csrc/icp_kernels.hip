@@ -42,9 +42,9 @@ __device__ int g_icp_status;                // nonzero: some pair was outside it
 // two reduction slabs of 16 doubles per wave at the front of the dynamic LDS
 // (block_sum_exact16, alternating between iterations), then 16 doubles of
 // per-pair constants (kept in LDS, not in registers across the NN search)
-constexpr int kPairConsts = 16;
+constexpr int kPairConsts = 32;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab
 __host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 16 + kPairConsts; }
-enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax };
+enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kBcast = 16 };
 
 struct IcpArgs {
     const double2* pts;
@@ -79,14 +79,13 @@ struct IcpArgs {
     float* sched_key;
     // gangs (GANG kernels only): a pair's query groups dealt over `gang`
     // workgroups on one XCD that exchange their per-iteration partial sums
-    // through gang_cnt / gang_slots; n_gangs pairs
+    // through gang_slots; n_gangs pairs
     int32_t gang;
     int32_t n_gangs;
-    uint32_t* gang_cnt;      // [n_gangs * kGangCntStride], zeroed before the launch
-    uint64_t* gang_slots;    // [n_gangs][2][gang][16] partial sums (fp64 bits)
+    uint64_t* gang_slots;    // [n_gangs][2][gang][32] tagged granules, zeroed before the launch
 };
-constexpr int kGangCntStride = 64;    // one 256-B line per gang counter
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
+constexpr int kGangSweep = 32;        // parts an exchange sweep covers (16 loads per lane)
 constexpr uint32_t kGangSpinLimit = 1u << 26;   // ~seconds of polling: a lost partner ends the launch
 __device__ int g_gang_timeout;        // set when a gang partner never arrived
 
@@ -376,7 +375,11 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             rl = fminf(rl, sqrtf(lb) * (1.0f - 1e-5f));
         }
         const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2[k];
+#ifdef SLAM_ABL_GROUP
+        act[k] = false;
+#else
         act[k] = valid[k] && !settled;
+#endif
         if (settled && sh != 0) st[k * st_stride] = st_pack(rl, ws[k]);
     }
     lap(1);
@@ -497,45 +500,219 @@ __device__ __forceinline__ bool certify(double d1, double s2, double a) {
     return s2 > fc;
 }
 
-// Gang exchange of one iteration's 16 exact partial sums (lane q of every wave
-// holds value q): wave 0 publishes this workgroup's slab with write-through
-// (sc1) stores, drains them and bumps the gang counter (agent scope); every
-// wave polls the counter (sc1 loads) until all `parts` slabs of exchange `e`
-// are in, then sums them in part order (the partials are exact sums on fixed
-// grids, so any order gives the same bits).  Slabs alternate by exchange
-// parity: a part can only reach exchange e + 2 after every part has arrived at
-// e + 1, i.e. after every part has read exchange e.  (MI355X_MICROARCH.md,
-// inter-workgroup visibility: sc1 stores + vmcnt(0) + agent atomic; sc1 poll
-// and sc1 payload loads.)
-__device__ __forceinline__ double gang_exchange(double t, uint32_t* cnt, uint64_t* slots, int part, int parts,
-                                                int e) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-    uint64_t* buf = slots + (e & 1) * parts * 16;
-    if (wave == 0) {
-        if (lane < 16)
-            __hip_atomic_store(buf + part * 16 + lane, static_cast<uint64_t>(__double_as_longlong(t)),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const uint32_t target = static_cast<uint32_t>(parts) * static_cast<uint32_t>(e + 1);
-    uint32_t spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+// One lane's share of a gang exchange sweep: granule g of parts pp, pp + 2, ...
+// (N per lane, addresses clamped so every load is issued unconditionally),
+// repeated until every tag matches; then the doubles reassembled across the
+// lane halves (lane l ^ 16 holds the other half) and summed.  Own granules come
+// from registers.
+template <int N>
+__device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp, int part, int parts, uint64_t tag,
+                                             uint32_t own, int lane) {
+    uint32_t v[N];
+    for (uint32_t spins = 0;;) {
+        uint64_t x[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            x[k] = __hip_atomic_load(buf + min(pp + 2 * k, parts - 1) * 32 + g, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const int p = pp + 2 * k;
+            v[k] = p == part ? own : static_cast<uint32_t>(x[k]);
+            ok &= p >= parts || p == part || (x[k] & 0xffffffff00000000ull) == tag;
+        }
+        if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > kGangSpinLimit) {   // a partner never arrived: flag it, end in finite time
             if (lane == 0) atomicOr(&g_gang_timeout, 1);
             break;
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool hi = (lane & 16) != 0;
     double s = 0.0;
-    if (lane < 16) {
-        for (int p = 0; p < parts; ++p)
-            s += __longlong_as_double(static_cast<long long>(
-                __hip_atomic_load(buf + p * 16 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v[k]), 16, 64));
+        const uint64_t bits = hi ? (static_cast<uint64_t>(v[k]) << 32) | other : (static_cast<uint64_t>(other) << 32) | v[k];
+        if (pp + 2 * k < parts) s += __longlong_as_double(static_cast<long long>(bits));
     }
     return s;
+}
+
+// Gang exchange of one iteration's 16 exact partial sums (lane q of every wave
+// holds value q) as data-tagged granules: the data IS the flag (guide R2).
+// Granule l < 32 of a part is the 8-byte {tag = e + 1, half (l >> 4) of value
+// (l & 15)}, written by ONE relaxed agent-scope (sc1) store; no drain, no
+// counter.  Every wave sweeps all parts' granules (sc1 loads, all in flight:
+// lane l reads granule l & 31 of parts l >> 5, (l >> 5) + 2, ...) until every
+// tag matches, then reassembles and sums them (the partials are exact sums on
+// fixed grids, so any order gives the same bits).  Slots alternate by
+// exchange parity: a part can only publish exchange e + 2 after reading every
+// part's e + 1 granules, each published after its reader finished exchange e.
+// (One exchange ~2 L2-miss round trips; the counter form it replaced took
+// four: store, drain, counter add, poll.)
+__device__ __forceinline__ double gang_exchange(double t, uint64_t* slots, int part, int parts, int e, double* bcast) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const uint64_t tag = static_cast<uint64_t>(e + 1) << 32;
+    uint64_t* buf = slots + (e & 1) * parts * 32;
+    const uint64_t tb = static_cast<uint64_t>(__double_as_longlong(__shfl(t, lane & 15, 64)));
+    if (wave == 0 && lane < 32)
+        __hip_atomic_store(buf + part * 32 + lane, tag | ((lane & 16) ? (tb >> 32) : (tb & 0xffffffffull)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) {   // one polling wave per workgroup (every wave polling queued the last arriver's loads)
+        const int g = lane & 31, pp = lane >> 5;
+        const uint32_t own = static_cast<uint32_t>((lane & 16) ? (tb >> 32) : tb);
+        double s = 0.0;
+        // branch-free sweeps of N loads per lane (a divergent guard around each
+        // load made the compiler drain them one by one)
+        if (parts <= 4)
+            s = gang_sweep<2>(buf, g, pp, part, parts, tag, own, lane);
+        else if (parts <= 8)
+            s = gang_sweep<4>(buf, g, pp, part, parts, tag, own, lane);
+        else if (parts <= 16)
+            s = gang_sweep<8>(buf, g, pp, part, parts, tag, own, lane);
+        else
+            s = gang_sweep<kGangSweep / 2>(buf, g, pp, part, parts, tag, own, lane);
+        s += __shfl_xor(s, 32, 64);   // parts of even + odd index (the same bits in both halves)
+        if (lane < 16) bcast[lane] = s;
+    }
+    // the slab is rewritten only at the next exchange, after the next
+    // block_sum_exact16 barrier, so every wave has read it by then
+    __syncthreads();
+    return lane < 16 ? bcast[lane] : 0.0;
+}
+
+// Per-pair setup shared by the kernels: pc2 into LDS (fp64, fp32 pairs with
+// far sentinels, sub-chunk boxes), max |coordinate| of both clouds, and the
+// per-pair constants in LDS (pconst): pc1's first point c, dp = sum(p - c) as an
+// order-free sum, pc1's centroid, the sum grids.  Ends with a barrier.
+struct PairSetup {
+    double cmax, pmaxd;
+    float pmax;
+    bool screen;
+    int nsub;
+};
+template <int BLOCK, bool SCREEN, bool PRUNE>
+__device__ __forceinline__ PairSetup stage_pair(const IcpArgs& a, int n1, int n2, const double2* __restrict__ p1,
+                                                const double2* __restrict__ p2, bool resident, double2* cand,
+                                                float2* candf, float4* box8, double* red0, double* red1,
+                                                double* pconst) {
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound, sum grids)
+    if (resident) {
+#pragma unroll kStageUnroll
+        for (int j = tid; j < n2; j += BLOCK) {   // unrolled: several loads in flight per thread
+            const double2 p = p2[j];
+            cand[j] = p;
+            if constexpr (SCREEN) cf_put(candf, j, static_cast<float>(p.x), static_cast<float>(p.y));
+            cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
+        }
+        if constexpr (SCREEN) {
+            for (int j = n2 + tid; j < (n2 + kChunk - 1) / kChunk * kChunk; j += BLOCK)
+                cf_put(candf, j, kSentinel, kSentinel);
+        }
+    } else {
+        for (int j = tid; j < n2; j += BLOCK) {
+            const double2 p = p2[j];
+            cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
+        }
+    }
+    const int nsub = (n2 + kChunk - 1) / kChunk * (kChunk / kSub);   // sub-chunks incl. padding
+    if constexpr (SCREEN && PRUNE) {
+        __syncthreads();   // candf complete
+        for (int c = tid; c < nsub; c += BLOCK) {
+            float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+            for (int j = c * kSub; j < min(n2, (c + 1) * kSub); ++j) {
+                const float2 p = cf_at(candf, j);
+                x0 = fminf(x0, p.x);
+                x1 = fmaxf(x1, p.x);
+                y0 = fminf(y0, p.y);
+                y1 = fmaxf(y1, p.y);
+            }
+            box8[c] = make_float4(x0, y0, x1, y1);
+        }
+    }
+    bool screen = false;
+    double pmaxd;        // max |coordinate| of pc1 (sum grids)
+    float pmax = 0.0f;   // PRUNE: the same in fp32 (motion bound slack)
+    {
+        double cm[2] = {cmax, 0.0};
+#pragma unroll kStageUnroll
+        for (int i = tid; i < n1; i += BLOCK) {
+            const double2 p = p1[i];
+            cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));
+        }
+        // block max through the second slab: max is exact, order-free
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            cm[0] = fmax(cm[0], __shfl_xor(cm[0], off, 64));
+            cm[1] = fmax(cm[1], __shfl_xor(cm[1], off, 64));
+        }
+        if (lane == 0) {
+            red1[wave] = cm[0];
+            red1[WAVES + wave] = cm[1];
+        }
+        __syncthreads();
+        cmax = red1[0];
+        double pm = red1[WAVES];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) {
+            cmax = fmax(cmax, red1[w]);
+            pm = fmax(pm, red1[WAVES + w]);
+        }
+        cmax = uniform_d(cmax);
+        pmaxd = uniform_d(pm);
+        pmax = uniform_f(static_cast<float>(pm) * (1.0f + 1e-6f));
+        // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
+        if constexpr (SCREEN) screen = cmax < 1e18;
+    }
+    // Cross-covariance centre: pc1's first point c (any per-pair constant
+    // works; it only keeps the terms small) and dp = sum(p - c), once per pair
+    // as an order-free sum (first slab; iteration 0 reduces into the second).
+    const double2 pc = p1[0];
+    double dpx, dpy;
+    {
+        const RsumGrid gp = rsum_grid(2.0 * pmaxd * (1.0 + 1e-12), n1);
+        double acc[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+        for (int i = tid; i < n1; i += BLOCK) {
+            const double2 p = p1[i];
+            rsum_add(p.x - pc.x, gp, acc[0], acc[1]);
+            rsum_add(p.y - pc.y, gp, acc[2], acc[3]);
+        }
+        const double t = block_sum_exact16<WAVES>(acc, red0);
+        dpx = readlane_d(t, 0) + readlane_d(t, 1);
+        dpy = readlane_d(t, 2) + readlane_d(t, 3);
+    }
+    if (tid == 0) {   // read back after the barrier before the loop
+        pconst[kPcX] = pc.x;
+        pconst[kPcY] = pc.y;
+        pconst[kDpX] = dpx;
+        pconst[kDpY] = dpy;
+        pconst[kMupX] = pc.x + dpx / static_cast<double>(n1);   // pc1's centroid: mu_p = c + dp / n
+        pconst[kMupY] = pc.y + dpy / static_cast<double>(n1);
+        const RsumGrid gm = rsum_grid(cmax, n1);                         // matched pc2 coordinates
+        const RsumGrid gs = rsum_grid(2.0 * pmaxd * cmax * (1.0 + 1e-12), n1);   // (p - c) m^T terms
+        pconst[kGm1] = gm.m1;
+        pconst[kGm2] = gm.m2;
+        pconst[kGs1] = gs.m1;
+        pconst[kGs2] = gs.m2;
+        pconst[kPmax] = pmaxd;
+        pconst[kCmax] = cmax;
+    }
+    __syncthreads();
+    PairSetup r;
+    r.cmax = cmax;
+    r.pmaxd = pmaxd;
+    r.pmax = pmax;
+    r.screen = screen;
+    r.nsub = nsub;
+    return r;
 }
 
 // DIAG: a diagnostics build of the kernel (per-phase s_memtime stamps of
@@ -613,40 +790,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         return;   // uniform
     }
 
-    double cmax = 0.0;   // max |coordinate| of pc2 (screen error bound, sum grids)
-    if (resident) {
-#pragma unroll kStageUnroll
-        for (int j = tid; j < n2; j += BLOCK) {   // unrolled: several loads in flight per thread
-            const double2 p = p2[j];
-            cand[j] = p;
-            if constexpr (SCREEN) cf_put(candf, j, static_cast<float>(p.x), static_cast<float>(p.y));
-            cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
-        }
-        if constexpr (SCREEN) {
-            for (int j = n2 + tid; j < (n2 + kChunk - 1) / kChunk * kChunk; j += BLOCK)
-                cf_put(candf, j, kSentinel, kSentinel);
-        }
-    } else {
-        for (int j = tid; j < n2; j += BLOCK) {
-            const double2 p = p2[j];
-            cmax = fmax(cmax, fmax(fabs(p.x), fabs(p.y)));
-        }
-    }
-    const int nsub = (n2 + kChunk - 1) / kChunk * (kChunk / kSub);   // sub-chunks incl. padding
-    if constexpr (SCREEN && PRUNE) {
-        __syncthreads();   // candf complete
-        for (int c = tid; c < nsub; c += BLOCK) {
-            float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
-            for (int j = c * kSub; j < min(n2, (c + 1) * kSub); ++j) {
-                const float2 p = cf_at(candf, j);
-                x0 = fminf(x0, p.x);
-                x1 = fmaxf(x1, p.x);
-                y0 = fminf(y0, p.y);
-                y1 = fmaxf(y1, p.y);
-            }
-            box8[c] = make_float4(x0, y0, x1, y1);
-        }
-    }
+    const PairSetup ps = stage_pair<BLOCK, SCREEN, PRUNE>(a, n1, n2, p1, p2, resident, cand, candf, box8, red0, red1,
+                                                          pconst);
+    const double cmax = ps.cmax;
+    const double pmaxd = ps.pmaxd;
+    const float pmax = ps.pmax;
+    const bool screen = ps.screen;
+    const int nsub = ps.nsub;
     int bprev[QPT];   // !PRUNE screen: last match in registers
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
@@ -657,75 +807,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         }
     }
     int nscan_total = 0;
-    bool screen = false;
-    double pmaxd;        // max |coordinate| of pc1 (sum grids)
-    float pmax = 0.0f;   // PRUNE: the same in fp32 (motion bound slack)
-    {
-        double cm[2] = {cmax, 0.0};
-#pragma unroll kStageUnroll
-        for (int i = tid; i < n1; i += BLOCK) {
-            const double2 p = p1[i];
-            cm[1] = fmax(cm[1], fmax(fabs(p.x), fabs(p.y)));
-        }
-        // block max through the second slab: max is exact, order-free
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            cm[0] = fmax(cm[0], __shfl_xor(cm[0], off, 64));
-            cm[1] = fmax(cm[1], __shfl_xor(cm[1], off, 64));
-        }
-        if (lane == 0) {
-            red1[wave] = cm[0];
-            red1[WAVES + wave] = cm[1];
-        }
-        __syncthreads();
-        cmax = red1[0];
-        double pm = red1[WAVES];
-#pragma unroll
-        for (int w = 1; w < WAVES; ++w) {
-            cmax = fmax(cmax, red1[w]);
-            pm = fmax(pm, red1[WAVES + w]);
-        }
-        cmax = uniform_d(cmax);
-        pmaxd = uniform_d(pm);
-        pmax = uniform_f(static_cast<float>(pm) * (1.0f + 1e-6f));
-        // finite fp32 squares guaranteed (SCREEN launches are LDS-resident)
-        if constexpr (SCREEN) screen = cmax < 1e18;
-    }
-    // Cross-covariance centre: pc1's first point c (any per-pair constant
-    // works; it only keeps the terms small) and dp = sum(p - c), once per pair
-    // as an order-free sum (first slab; iteration 0 reduces into the second).
-    const double2 pc = p1[0];
-    double dpx, dpy;
-    {
-        const RsumGrid gp = rsum_grid(2.0 * pmaxd * (1.0 + 1e-12), n1);
-        double acc[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-        for (int i = tid; i < n1; i += BLOCK) {
-            const double2 p = p1[i];
-            rsum_add(p.x - pc.x, gp, acc[0], acc[1]);
-            rsum_add(p.y - pc.y, gp, acc[2], acc[3]);
-        }
-        const double t = block_sum_exact16<WAVES>(acc, red0);
-        dpx = readlane_d(t, 0) + readlane_d(t, 1);
-        dpy = readlane_d(t, 2) + readlane_d(t, 3);
-    }
-    if (tid == 0) {   // read back after the barrier before the loop
-        pconst[kPcX] = pc.x;
-        pconst[kPcY] = pc.y;
-        pconst[kDpX] = dpx;
-        pconst[kDpY] = dpy;
-        pconst[kMupX] = pc.x + dpx / static_cast<double>(n1);   // pc1's centroid: mu_p = c + dp / n
-        pconst[kMupY] = pc.y + dpy / static_cast<double>(n1);
-        const RsumGrid gm = rsum_grid(cmax, n1);                         // matched pc2 coordinates
-        const RsumGrid gs = rsum_grid(2.0 * pmaxd * cmax * (1.0 + 1e-12), n1);   // (p - c) m^T terms
-        pconst[kGm1] = gm.m1;
-        pconst[kGm2] = gm.m2;
-        pconst[kGs1] = gs.m1;
-        pconst[kGs2] = gs.m2;
-        pconst[kPmax] = pmaxd;
-        pconst[kCmax] = cmax;
-    }
     // PRUNE: this iteration's motion T - T_prev in fp32 and its rounding slack
     float dT[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dsig = 0.0f;
     const int n2_pad = (n2 + kChunk - 1) / kChunk * kChunk;
@@ -894,7 +975,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const double s2 = static_cast<double>(fminf(M2[k], b2));   // every other j: d32 >= s2
                         const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
                         const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
+#ifdef SLAM_ABL_CERT
+                        ok = true;
+#else
                         ok = cq < 1e18 && s2 < 3.0e38 && certify(d1, s2, ab);
+#endif
                     }
                     // wave-cooperative exact fp64 scan for each uncertified query of
                     // this group: the whole wave scans pc2 for it, a (distance, index)
@@ -1023,8 +1108,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         }
         if constexpr (GANG) {
             if (parts > 1)
-                tot = gang_exchange(tot, a.gang_cnt + static_cast<int64_t>(slot) * kGangCntStride,
-                                    a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 16, part, parts, it - it0);
+                tot = gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part, parts,
+                                    it - it0, pconst + kBcast);
         }
         const double n = static_cast<double>(n1);
         const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
@@ -1126,6 +1211,423 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 }
                 return;
             }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Team kernel (latency mode for the strong-scaling tail).  A gang of
+// workgroups runs one pair, ONE 64-query group per workgroup, and the
+// group's search is split over the kTeam waves of its workgroup: wave w scans
+// window sub-chunk ws + w and every kTeam-th batch of the live sub-chunks, the
+// partial top-2 results meet in LDS (merged in wave order: the window's
+// left-to-right order).  A lone pair's iteration is then about a quarter of
+// its slowest group's search plus the exchanges, instead of the whole group's
+// (one outlier group — queries far from every candidate, 70-110 live
+// sub-chunks — set the lone latency).  Every wave holds
+// the same 64 queries and their state (matches, clearances) in registers and
+// updates it identically; wave 0 alone contributes the sums.  Results equal
+// the one-workgroup kernels bit for bit (same exact sums, same winners).
+// ---------------------------------------------------------------------------
+#ifndef SLAM_TEAM_WAVES
+#define SLAM_TEAM_WAVES 4
+#endif
+constexpr int kTeam = SLAM_TEAM_WAVES;   // waves per query group (lone pair 1118: 4 waves 12.5 us/iter, 8 waves 13.0: the
+                                         // merges, barriers and sums grow faster than the slowest group's search shrinks)
+constexpr int kTeamMaxParts = kGangSweep;   // query groups of a team-run pair (2,048 points)
+constexpr int kTeamBlock = 64 * kTeam;
+
+// (M1, J1, M2) <- the top-2 of itself and (m1, j1, m2), both sorted; ties keep
+// the current J1 (earlier in visit order), as take_cand does
+__device__ __forceinline__ void top2_merge(float& M1, float& M2, int& J1, float m1, float m2, int j1) {
+    const uint32_t a1 = __float_as_uint(M1), a2 = __float_as_uint(M2);
+    const uint32_t b1 = __float_as_uint(m1), b2 = __float_as_uint(m2);
+    J1 = b1 < a1 ? j1 : J1;
+    M2 = __uint_as_float(min(max(a1, b1), min(a2, b2)));
+    M1 = __uint_as_float(min(a1, b1));
+}
+
+__host__ __device__ constexpr size_t team_xbuf_words() { return 2 * kTeam * 4 * 64; }
+
+__global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
+    constexpr int WAVES = kTeam;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* red0 = reinterpret_cast<double*>(smem);
+    double* red1 = red0 + WAVES * 16;
+    double* pconst = red0 + 2 * WAVES * 16;
+    double2* cand = reinterpret_cast<double2*>(smem + red_doubles(kTeamBlock) * sizeof(double));
+    const int cap = a.cand_cap;
+    float2* candf = reinterpret_cast<float2*>(cand + cap);
+    float4* box8 = reinterpret_cast<float4*>(candf + cap);
+    uint32_t* xbuf = reinterpret_cast<uint32_t*>(box8 + cap / kSub);   // [2][kTeam][4][64] merge slots
+
+    const int parts = a.gang;
+    const int bx = static_cast<int>(blockIdx.x);
+    const int slot = (bx / (8 * parts)) * 8 + (bx & 7);
+    const int part = (bx >> 3) % parts;   // = the query group of this workgroup
+    if (slot >= a.n_gangs) return;
+    const int b = a.order ? a.order[slot] : slot;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int it0 = 0;
+    if (a.resume) {
+        const int s = a.out_iters[b];
+        if (s > 0 || s == kBadBounds) return;
+        it0 = -s;
+    }
+    const int s1 = a.src_scan[b];
+    const int s2 = a.dst_scan[b];
+    const int64_t o1 = a.scan_off[s1];
+    const int64_t o2 = a.scan_off[s2];
+    const int n1 = static_cast<int>(a.scan_off[s1 + 1] - o1);
+    const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
+    const double2* __restrict__ p1 = a.pts + o1;
+    const double2* __restrict__ p2 = a.pts + o2;
+    if (n1 < 1 || n2 < 1 || n1 > 64 * parts || n2 > cap) {
+        if (tid == 0 && part == 0) {
+            a.out_iters[b] = kBadBounds;
+            a.out_err[b] = __builtin_nan("");
+            atomicOr(&g_icp_status, 1);
+        }
+        return;
+    }
+    const PairSetup ps = stage_pair<kTeamBlock, true, true>(a, n1, n2, p1, p2, true, cand, candf, box8, red0, red1,
+                                                            pconst);
+    const int nsub = ps.nsub;
+    const bool screen = ps.screen;
+    SE2 T = load_se2((it0 > 0 ? a.out_tf : a.init) + 9 * static_cast<int64_t>(b));
+    if (a.rotation_only) {
+        T.m02 = 0.0;
+        T.m12 = 0.0;
+    }
+    double* hist = a.hist_stride > 0 ? a.out_hist + static_cast<int64_t>(b) * a.hist_stride * 9 : nullptr;
+    if (hist && tid == 0 && part == 0 && it0 == 0) store_se2(hist, T);
+    double last_err = it0 > 0 ? a.out_err[b] : 0.0;
+    float dT[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dsig = 0.0f;
+    int prev = -1;      // last match (identical in every wave)
+    uint32_t st = 0;    // clearance word (radius | window start), see st_pack
+    const int i = part * 64 + lane;
+    const bool valid = i < n1;
+    const int nw = (nsub + 63) >> 6;
+    // diagnostics (a.stamps != NULL): s_memtime per phase of wave 0 of every part,
+    // stamps[256 + 16 * part + phase]
+    const bool stamping = a.stamps != nullptr && wave == 0;
+    unsigned long long tp = stamping ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    auto tstamp = [&](int q) {
+        if (stamping) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            tacc[q] += t1 - tp;
+            tp = t1;
+        }
+    };
+    auto tflush = [&]() {
+        if (stamping && lane == 0)
+            for (int q = 0; q < 10; ++q) atomicAdd(a.stamps + 256 + 16 * part + q, tacc[q]);
+    };
+    for (int it = it0;; ++it) {
+        double x = 0.0, y = 0.0;
+        if (valid) {
+            const double2 p = p1[i];
+            x = p.x;
+            y = p.y;
+        }
+        const double qx = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));
+        const double qy = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+        const float fx = static_cast<float>(qx), fy = static_cast<float>(qy);
+        {   // carried clearance minus this iteration's motion (as icp_kernel)
+            const float xf = static_cast<float>(x), yf = static_cast<float>(y);
+            const float ex = fmaf(dT[1], yf, fmaf(dT[0], xf, dT[2]));
+            const float ey = fmaf(dT[4], yf, fmaf(dT[3], xf, dT[5]));
+            const float dl = (sqrtf(fmaf(ey, ey, ex * ex)) + 1e-6f * (fabsf(fx) + fabsf(fy) + fabsf(ex) + fabsf(ey)) +
+                              dsig) * (1.0f + 1e-5f);
+            st = st_pack((st_radius(st) - dl) * (1.0f - 1e-5f), st_ws(st));
+        }
+        float M1 = INFINITY, M2 = INFINITY;
+        int J1 = 0;
+        int ws = 0;
+        bool act = false;
+        float lmin = INFINITY, gfar = INFINITY;
+        uint32_t* xb = xbuf + (it & 1) * (kTeam * 4 * 64);
+        if (screen) {
+            const int pred = prev >= 0 ? prev : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
+            {
+                const int lo = kWin / 2 - ((pred & (kSub - 1)) >= kSub / 2 ? 1 : 0);
+                ws = min(max((pred >> 3) - lo, 0), nsub - kWin);
+            }
+            // window: this wave's sub-chunk ws + wave (waves past the window: none)
+            if (wave < kWin) {
+                const int c8 = (ws + wave) * kSub;
+#pragma unroll
+                for (int t = 0; t < kSub; t += 2) {
+                    const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
+                    const f32x2v d = screen_pair(pp, fx, fy);
+                    take_cand(d.x, c8 + t, M1, M2, J1);
+                    take_cand(d.y, c8 + t + 1, M1, M2, J1);
+                }
+            }
+            tstamp(0);
+            xb[(wave * 4 + 0) * 64 + lane] = __float_as_uint(M1);
+            xb[(wave * 4 + 1) * 64 + lane] = static_cast<uint32_t>(J1);
+            xb[(wave * 4 + 2) * 64 + lane] = __float_as_uint(M2);
+            __syncthreads();
+            tstamp(1);
+            M1 = INFINITY;
+            M2 = INFINITY;
+            J1 = 0;
+#pragma unroll
+            for (int w = 0; w < kTeam; ++w)
+                top2_merge(M1, M2, J1, __uint_as_float(xb[(w * 4 + 0) * 64 + lane]),
+                           __uint_as_float(xb[(w * 4 + 2) * 64 + lane]), static_cast<int>(xb[(w * 4 + 1) * 64 + lane]));
+            // clearance test (identical in every wave)
+            {
+                const int wp = st_ws(st);
+                const int sh = ws - wp;
+                float rl = st_radius(st);
+                if (sh != 0) {
+                    const int c0 = sh > 0 ? wp : wp + kWin - 1;
+                    const int c1 = sh > 0 ? wp + 1 : wp + kWin - 2;
+                    const float4 b0 = box8[min(max(c0, 0), nsub - 1)];
+                    const float4 b1 = box8[min(max(c1, 0), nsub - 1)];
+                    float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, b0);
+                    if (sh * sh > 1) lb = fminf(lb, box_lb(f32x2{fx, fy}, f32x2{fx, fy}, b1));
+                    rl = fminf(rl, sqrtf(lb) * (1.0f - 1e-5f));
+                }
+                const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2;
+                act = valid && !settled;
+                if (settled && sh != 0) st = st_pack(rl, ws);
+            }
+            tstamp(2);
+            // group search past the window, split over the team
+            float E1 = INFINITY, E2 = INFINITY;
+            int EJ = 0;
+            if (__ballot(act) != 0) {   // identical in every wave
+                const float bx0 = wave_min_f(act ? fx : INFINITY);
+                const float bx1 = wave_max_f(act ? fx : -INFINITY);
+                const float by0 = wave_min_f(act ? fy : INFINITY);
+                const float by1 = wave_max_f(act ? fy : -INFINITY);
+                const float gM2 = wave_max_f(act ? M2 : -INFINITY);
+                float gf = INFINITY;
+                int bcount = 0;
+                for (int w = 0; w < nw; ++w) {
+                    const int sl = 64 * w + lane;
+                    const float glb = box_lb(f32x2{bx0, by0}, f32x2{bx1, by1}, box8[min(sl, nsub - 1)]);
+                    const bool gl = glb <= gM2;
+                    gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
+                    uint64_t live = __ballot((sl < nsub) & gl);
+                    while (live) {
+                        uint64_t scpack = 0;
+                        uint32_t has = 0;
+                        float4 bb[kBatch];
+#pragma unroll
+                        for (int u = 0; u < kBatch; ++u) {
+                            const int pos = live ? static_cast<int>(__builtin_ctzll(live)) : 0;
+                            has |= static_cast<uint32_t>(live != 0) << u;
+                            live &= live - 1;
+                            scpack |= static_cast<uint64_t>(pos) << (6 * u);
+                            bb[u] = box8[64 * w + pos];
+                        }
+                        const bool mine = (bcount++ % kTeam) == wave;   // wave-uniform
+                        if (!mine) continue;
+                        // current upper bound of the final M2: second smallest of the
+                        // window's top-2 and this wave's extra top-2
+                        const uint32_t m2l = min(max(__float_as_uint(M1), __float_as_uint(E1)),
+                                                 min(__float_as_uint(M2), __float_as_uint(E2)));
+                        uint32_t need = 0;
+#pragma unroll
+                        for (int u = 0; u < kBatch; ++u) {
+                            const int sc = 64 * w + static_cast<int>((scpack >> (6 * u)) & 63);
+                            const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, bb[u]);
+                            const bool out = (sc < ws) | (sc >= ws + kWin);
+                            lmin = out ? fminf(lmin, lb) : lmin;
+                            need |= static_cast<uint32_t>(act & out & (lb <= __uint_as_float(m2l))) << u;
+                        }
+                        need &= has;
+                        uint32_t todo = wave_or_u32(need);
+                        while (todo) {
+                            const int u = __builtin_ctz(todo);
+                            todo &= todo - 1;
+                            const int c8 = (64 * w + static_cast<int>((scpack >> (6 * u)) & 63)) * kSub;
+                            if ((need >> u) & 1u) {
+#pragma unroll
+                                for (int t = 0; t < kSub; t += 2) {
+                                    const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
+                                    const f32x2v d = screen_pair(pp, fx, fy);
+                                    take_cand(d.x, c8 + t, E1, E2, EJ);
+                                    take_cand(d.y, c8 + t + 1, E1, E2, EJ);
+                                }
+                            }
+                        }
+                    }
+                }
+                gfar = wave_min_f(gf);
+            }
+            // merge the team's extra candidates (disjoint from the window and from
+            // each other) and the clearance bounds
+            uint32_t* xb2 = xb + 0;   // second half of this iteration's slots
+            xb2 = xbuf + ((it & 1) ^ 1) * (kTeam * 4 * 64);
+            xb2[(wave * 4 + 0) * 64 + lane] = __float_as_uint(E1);
+            xb2[(wave * 4 + 1) * 64 + lane] = static_cast<uint32_t>(EJ);
+            xb2[(wave * 4 + 2) * 64 + lane] = __float_as_uint(E2);
+            xb2[(wave * 4 + 3) * 64 + lane] = __float_as_uint(lmin);
+            tstamp(3);
+            __syncthreads();
+            tstamp(4);
+            float lm = INFINITY;
+#pragma unroll
+            for (int w = 0; w < kTeam; ++w) {
+                top2_merge(M1, M2, J1, __uint_as_float(xb2[(w * 4 + 0) * 64 + lane]),
+                           __uint_as_float(xb2[(w * 4 + 2) * 64 + lane]), static_cast<int>(xb2[(w * 4 + 1) * 64 + lane]));
+                lm = fminf(lm, __uint_as_float(xb2[(w * 4 + 3) * 64 + lane]));
+            }
+            if (act) st = st_pack(sqrtf(fminf(gfar, lm)) * (1.0f - 1e-5f), ws);
+        }
+        tstamp(5);
+        // certification (identical in every wave) and the exact fallback
+        int bi;
+        {
+            const int j1 = min(J1, n2 - 1);
+            bi = j1;
+            bool ok = true;
+            if (!screen) {
+                ok = !valid;
+            } else if (valid && n2 > 1) {
+                const double2 c = cand[j1];
+                const double d1 = exact_d2(c.x, c.y, qx, qy);
+                const double cq = fmax(fabs(qx), fabs(qy));
+                const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (ps.cmax + cq);
+                ok = cq < 1e18 && M2 < 3.0e38f && certify(d1, static_cast<double>(M2), ab);
+            }
+            uint64_t fails = __ballot(!ok);
+            while (fails) {
+                const int src = static_cast<int>(__builtin_ctzll(fails));
+                fails &= fails - 1;
+                const double xs = bcast_d(qx, src), ys = bcast_d(qy, src);
+                double bd = INFINITY;
+                int bj = lane < n2 ? lane : 0x7fffffff;
+                for (int j = lane; j < n2; j += 64) {
+                    const double2 c = cand[j];
+                    const double d = exact_d2(c.x, c.y, xs, ys);
+                    if (d < bd) {
+                        bd = d;
+                        bj = j;
+                    }
+                }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const double od = __shfl_xor(bd, off, 64);
+                    const int oj = __shfl_xor(bj, off, 64);
+                    if (od < bd || (od == bd && oj < bj)) {
+                        bd = od;
+                        bj = oj;
+                    }
+                }
+                if (lane == src) bi = bj;
+            }
+            prev = valid ? bi : -1;
+        }
+        tstamp(6);
+        // sums: wave 0's 64 queries (the other waves hold the same ones)
+        double tot;
+        {
+            const double2 c = *reinterpret_cast<const double2*>(pconst + kPcX);
+            const double2 gmv = *reinterpret_cast<const double2*>(pconst + kGm1);
+            const double2 gsv = *reinterpret_cast<const double2*>(pconst + kGs1);
+            const double2 pcm = *reinterpret_cast<const double2*>(pconst + kPmax);
+            const double bq = (fmax(fabs(T.m00) + fabs(T.m01), fabs(T.m10) + fabs(T.m11)) * pcm.x +
+                               fmax(fabs(T.m02), fabs(T.m12))) * (1.0 + 1e-12);
+            const RsumGrid gm{gmv.x, gmv.y}, gs{gsv.x, gsv.y};
+            const RsumGrid gd = rsum_grid(2.0 * (bq + pcm.y) * (bq + pcm.y) * (1.0 + 1e-12), n1);
+            double acc[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+            if (wave == 0 && valid) {
+                const double2 m = cand[bi];
+                rsum_add(m.x, gm, acc[0], acc[1]);
+                rsum_add(m.y, gm, acc[2], acc[3]);
+                rsum_add(exact_d2(m.x, m.y, qx, qy), gd, acc[4], acc[5]);
+                const double ax = x - c.x, ay = y - c.y;
+                rsum_add(ax * m.x, gs, acc[6], acc[7]);
+                rsum_add(ax * m.y, gs, acc[8], acc[9]);
+                rsum_add(ay * m.x, gs, acc[10], acc[11]);
+                rsum_add(ay * m.y, gs, acc[12], acc[13]);
+            }
+            tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
+            tstamp(7);
+            if (parts > 1)
+                tot = gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part, parts,
+                                    it - it0, pconst + kBcast);
+        }
+        tstamp(8);
+        const double n = static_cast<double>(n1);
+        const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;
+        const double mvy = (readlane_d(tot, 2) + readlane_d(tot, 3)) / n;
+        const double err = readlane_d(tot, 4) + readlane_d(tot, 5);
+        const double2 dp = *reinterpret_cast<const double2*>(pconst + kDpX);
+        const double2 mup = *reinterpret_cast<const double2*>(pconst + kMupX);
+        const double mux = fma(T.m02, 1.0, fma(T.m01, mup.y, T.m00 * mup.x));
+        const double muy = fma(T.m12, 1.0, fma(T.m11, mup.y, T.m10 * mup.x));
+        const double p00 = fma(-dp.x, mvx, readlane_d(tot, 6) + readlane_d(tot, 7));
+        const double p01 = fma(-dp.x, mvy, readlane_d(tot, 8) + readlane_d(tot, 9));
+        const double p10 = fma(-dp.y, mvx, readlane_d(tot, 10) + readlane_d(tot, 11));
+        const double p11 = fma(-dp.y, mvy, readlane_d(tot, 12) + readlane_d(tot, 13));
+        const double s00 = fma(T.m01, p10, T.m00 * p00);
+        const double s01 = fma(T.m01, p11, T.m00 * p01);
+        const double s10 = fma(T.m11, p10, T.m10 * p00);
+        const double s11 = fma(T.m11, p11, T.m10 * p01);
+        const double cs = s00 + s11;
+        const double sn = s01 - s10;
+        const double r = sqrt(cs * cs + sn * sn);
+        const double co = r > 0.0 ? cs / r : 1.0;
+        const double si = r > 0.0 ? sn / r : 0.0;
+        double tx = mvx - fma(-si, muy, co * mux);
+        double ty = mvy - fma(co, muy, si * mux);
+        if (a.rotation_only) {
+            tx = 0.0;
+            ty = 0.0;
+        }
+        SE2 D;
+        D.m00 = co; D.m01 = -si; D.m02 = tx;
+        D.m10 = si; D.m11 = co;  D.m12 = ty;
+        const SE2 Tn = se2_mul(D, T);
+        if (hist && tid == 0 && part == 0) store_se2(hist + 9 * (it + 1), Tn);
+        const double derr = fabs(last_err - err);
+        const bool stop = (err < a.epsilon) || (it > a.max_iters) || (it > 0 && derr < a.stopping_thresh);
+        last_err = err;
+        dT[0] = uniform_f(static_cast<float>(Tn.m00 - T.m00));
+        dT[1] = uniform_f(static_cast<float>(Tn.m01 - T.m01));
+        dT[2] = uniform_f(static_cast<float>(Tn.m02 - T.m02));
+        dT[3] = uniform_f(static_cast<float>(Tn.m10 - T.m10));
+        dT[4] = uniform_f(static_cast<float>(Tn.m11 - T.m11));
+        dT[5] = uniform_f(static_cast<float>(Tn.m12 - T.m12));
+        {
+            const float rr = fmaxf(fabsf(dT[0]) + fabsf(dT[1]), fabsf(dT[3]) + fabsf(dT[4]));
+            const float tt = fmaxf(fabsf(dT[2]), fabsf(dT[5]));
+            const float big = static_cast<float>(fabs(T.m02) + fabs(T.m12) + fabs(Tn.m02) + fabs(Tn.m12));
+            dsig = uniform_f(1e-6f * (rr * ps.pmax + tt) + 1e-9f * (ps.pmax + big) + 1e-30f);
+        }
+        T.m00 = uniform_d(Tn.m00); T.m01 = uniform_d(Tn.m01); T.m02 = uniform_d(Tn.m02);
+        T.m10 = uniform_d(Tn.m10); T.m11 = uniform_d(Tn.m11); T.m12 = uniform_d(Tn.m12);
+        tstamp(9);
+        if (stop) {
+            tflush();
+            if (tid == 0 && part == 0) {
+                store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                a.out_err[b] = err;
+                a.out_iters[b] = it + 1;
+            }
+            return;
+        }
+        if (a.phase_cap > 0 && it + 1 - it0 >= a.phase_cap) {
+            tflush();
+            if (tid == 0 && part == 0) {
+                store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                a.out_err[b] = err;
+                a.out_iters[b] = -(it + 1);
+                a.sched_key[b] = static_cast<float>(derr);
+            }
+            return;
         }
     }
 }
@@ -1374,12 +1876,30 @@ static SideStream* side_stream(int dev) {
     return &e;
 }
 
-// G pairs (args.order[0..G)) as gangs of `parts` workgroups; cnt (G x
-// kGangCntStride uint32, zeroed on `s` before this) and slots (G x 2 x parts x
-// 16 uint64) are stream-ordered workspace.  Every gang's parts must be
+// G pairs (args.order[0..G)) as gangs of `parts` workgroups; slots (G x 2 x
+// parts x 32 uint64 granules, zeroed on `s` before this) are stream-ordered
+// workspace.  Every gang's parts must be
 // co-resident: G * parts workgroups of one CU each stay far below the CU count.
-static int launch_gangs(const IcpArgs& args, int G, int parts, int max_n1, int max_n2, hipStream_t s,
-                        uint32_t* cnt, uint64_t* slots) {
+static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int max_n1, int max_n2, hipStream_t s,
+                        uint64_t* slots) {
+    if (team) {   // one query group per workgroup, the group's search split over its kTeam waves
+        if (max_n2 > kCandCap || parts < 1 || parts > kTeamMaxParts) return fail(SLAM_EINVAL, "icp teams: shape");
+        IcpArgs a = args;
+        a.stamps = g_icp_stamps;   // diagnostics: per-part phase cycles (icp_team_kernel)
+        a.evals = nullptr;
+        a.cand_cap = ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk;
+        a.gang = parts;
+        a.n_gangs = G;
+        a.gang_slots = slots;
+        const size_t lds_need = red_doubles(kTeamBlock) * sizeof(double) +
+                                static_cast<size_t>(a.cand_cap) * (sizeof(double2) + sizeof(float2)) +
+                                static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) + team_xbuf_words() * sizeof(uint32_t);
+        if (lds_need > kMaxLds) return fail(SLAM_EINVAL, "icp teams: LDS");
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(icp_team_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxLds));
+        hipLaunchKernelGGL(icp_team_kernel, dim3((G + 7) / 8 * 8 * parts), dim3(kTeamBlock), kMaxLds, s, a);
+        return check_launch("icp team kernel");
+    }
     const GangInstance* gi = pick_gang_instance(max_n1, parts);
     if (!gi || parts < 2 || parts > kGangMax || max_n2 > kCandCap) return fail(SLAM_EINVAL, "icp gangs: no instance");
     IcpArgs a = args;
@@ -1388,7 +1908,6 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, int max_n1, int m
     a.cand_cap = ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk;
     a.gang = parts;
     a.n_gangs = G;
-    a.gang_cnt = cnt;
     a.gang_slots = slots;
     const size_t lds_need = red_doubles(gi->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2) +
                             static_cast<size_t>(a.cand_cap) * sizeof(float2) +
@@ -1445,22 +1964,23 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     // tiers of phase 2: gangs (order[0, G)), CU-exclusive heads (order[G, H)),
     // the rest (order[H, B)) beside them
     const int heads = g_sched_heads > 0 && B < kHeadsMaxPairs ? min(g_sched_heads, max(B / 16, 1)) : 0;
-    const int parts = g_sched_gang_parts;
-    const bool gang_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap && parts >= 2 &&
-                         pick_gang_instance(max_n1, parts) != nullptr;
+    // gang parts: g_sched_gang_parts workgroups per pair, or (0) teams: one
+    // workgroup per 64-query group
+    const bool team = g_sched_gang_parts == 0;
+    const int parts = team ? (max_n1 + 63) / 64 : g_sched_gang_parts;
+    const bool gang_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap &&
+                         (team ? parts <= kTeamMaxParts : parts >= 2 && pick_gang_instance(max_n1, parts) != nullptr);
     const int G = gang_ok ? min(g_sched_gangs, heads) : 0;
-    const size_t gang_cnt_bytes = static_cast<size_t>(G) * kGangCntStride * sizeof(uint32_t);
-    const size_t gang_slot_bytes = static_cast<size_t>(G) * 2 * max(parts, 1) * 16 * sizeof(uint64_t);
+    const size_t gang_slot_bytes = static_cast<size_t>(G) * 2 * max(parts, 1) * 32 * sizeof(uint64_t);
     const size_t sched_bytes = ((kSchedBuckets + 1) * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float)) + 255) / 256 * 256;
-    const size_t bytes = sched_bytes + gang_cnt_bytes + gang_slot_bytes;
+    const size_t bytes = sched_bytes + gang_slot_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);
     int32_t* bucket = hist + kSchedBuckets + 1;
     int32_t* order = bucket + nb;
     float* key = reinterpret_cast<float*>(order + nb);
-    uint32_t* gang_cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + sched_bytes);
-    uint64_t* gang_slots = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes + gang_cnt_bytes);
+    uint64_t* gang_slots = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes);
     IcpArgs a = args;
     a.phase_cap = probe;
     a.sched_key = key;
@@ -1469,7 +1989,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         const int g = (B + 255) / 256;
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
         (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
-        if (G > 0) (void)hipMemsetAsync(gang_cnt, 0, gang_cnt_bytes, s);
+        if (G > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
         hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
         hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);
         hipLaunchKernelGGL(sched_scatter_kernel, dim3(g), dim3(256), 0, s, bucket, B, hist, order);
@@ -1493,7 +2013,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess ||
                 hipStreamWaitEvent(side->stream2, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
-            if (rc == 0 && G > 0) rc = launch_gangs(a, G, parts, max_n1, max_n2, s, gang_cnt, gang_slots);
+            if (rc == 0 && G > 0) rc = launch_gangs(a, G, parts, team, max_n1, max_n2, s, gang_slots);
             if (rc == 0 && H > G) {
                 IcpArgs h = a;
                 h.order = order + G;
@@ -1558,7 +2078,8 @@ int slam_icp_set_schedule_heads(int heads) {
     return ok();
 }
 int slam_icp_set_schedule_gangs(int gangs, int parts) {
-    if (gangs < 0 || parts < 2 || parts > kGangMax) return fail(SLAM_EINVAL, "schedule: gangs %d parts %d", gangs, parts);
+    if (gangs < 0 || parts == 1 || parts < 0 || parts > kGangMax)
+        return fail(SLAM_EINVAL, "schedule: gangs %d parts %d", gangs, parts);
     g_sched_gangs = gangs;
     g_sched_gang_parts = parts;
     return ok();

@@ -93,28 +93,6 @@ __device__ __forceinline__ M3 m3_inv(const M3& m) {
     return r;
 }
 
-// Closed-form 3x3 inverse (adjugate times one reciprocal of the determinant):
-// the relaxation's dependent chain keeps one fp64 division instead of the
-// nine of the pivoted LU (agrees with it to rounding; tests at 1e-9).
-__device__ __forceinline__ M3 m3_inv_adj(const M3& m) {
-    const double(&a)[3][3] = m.a;
-    const double c00 = fma(a[1][1], a[2][2], -a[1][2] * a[2][1]);
-    const double c01 = fma(a[1][2], a[2][0], -a[1][0] * a[2][2]);
-    const double c02 = fma(a[1][0], a[2][1], -a[1][1] * a[2][0]);
-    const double id = 1.0 / fma(a[0][0], c00, fma(a[0][1], c01, a[0][2] * c02));
-    M3 r;
-    r.a[0][0] = c00 * id;
-    r.a[1][0] = c01 * id;
-    r.a[2][0] = c02 * id;
-    r.a[0][1] = fma(a[0][2], a[2][1], -a[0][1] * a[2][2]) * id;
-    r.a[1][1] = fma(a[0][0], a[2][2], -a[0][2] * a[2][0]) * id;
-    r.a[2][1] = fma(a[0][1], a[2][0], -a[0][0] * a[2][1]) * id;
-    r.a[0][2] = fma(a[0][1], a[1][2], -a[0][2] * a[1][1]) * id;
-    r.a[1][2] = fma(a[0][2], a[1][0], -a[0][0] * a[1][2]) * id;
-    r.a[2][2] = fma(a[0][0], a[1][1], -a[0][1] * a[1][0]) * id;
-    return r;
-}
-
 // construct_R (src/pose_graph_optimization.py:76-85)
 __device__ __forceinline__ M3 rot_z(double theta) {
     double s, c;
@@ -208,10 +186,16 @@ __global__ void sgd_weights_kernel(int32_t N, const int32_t* __restrict__ A, con
 }
 
 constexpr int kRelaxBlock = 512;
-#ifndef SLAM_RELAX_THREADS
-#define SLAM_RELAX_THREADS 256
-#endif
-constexpr int kRelaxThreads = SLAM_RELAX_THREADS;   // the relaxation workgroup: one wave per SIMD (512: 14.9 ms/step at C4, 256: 13.1, 128: 13.0)
+// The relaxation workgroup: poses in LDS -> ONE wave (LDS operations of a wave
+// complete in order: no barriers, no read-count protocol, and every LDS read of
+// an edge's updates in flight at once); poses in global memory -> 256 threads
+// with the workgroup protocol (512: 14.9 ms/step at C4, 256: 13.1, 128: 13.0
+// before the one-wave path).
+template <bool IN_LDS>
+constexpr int relax_threads() {
+    return IN_LDS ? 64 : 256;
+}
+constexpr int kRelaxSlots = 2;   // explicit nodes per thread with prefetched C values
 
 // Inclusive prefix sums of 1/M per column: C[0] = 0, C[i+1] = C[i] + invM[i].
 // One workgroup, chunked block scan (fixed order).  The relaxation then reads
@@ -258,6 +242,18 @@ __global__ __launch_bounds__(kRelaxBlock) void sgd_prefix_kernel(const double* _
             run[j] += w(i, j);
             C[3 * (i + 1) + j] = run[j];
         }
+}
+
+// 1 / (C[b+1] - C[a+1]) per active edge (the ramp's reciprocal total weight;
+// pose-independent within a step), off the relaxation's sequential chain.
+__global__ void sgd_irtw_kernel(const int32_t* __restrict__ A, const int32_t* __restrict__ B,
+                                const int32_t* __restrict__ Kp, const double* __restrict__ C, int32_t E,
+                                double* __restrict__ RT) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= E || k >= *Kp) return;
+    const int a = A[k], b = B[k];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) RT[3 * k + j] = 1.0 / (C[3 * (b + 1) + j] - C[3 * (a + 1) + j]);
 }
 
 // Active loop edges (|a - b| != 1 and a < b: the edges pass 2 applies) in
@@ -324,11 +320,49 @@ __global__ __launch_bounds__(1024) void sgd_compact_kernel(const int32_t* __rest
 constexpr int kLdsPoses = 6144;
 constexpr int kMaxOffBlocks = 2048;
 
-template <bool IN_LDS>
-__global__ __launch_bounds__(kRelaxThreads) void sgd_relax_kernel(
-    double* __restrict__ g_poses, int32_t N, const int32_t* __restrict__ A, const int32_t* __restrict__ B,
-    const double* __restrict__ TF, const int32_t* __restrict__ Kp, const double* __restrict__ C,
-    const double* __restrict__ gamma, double lr, double sigma, int32_t sh) {
+// Diagnostics build (-DSLAM_SGD_STAMPS): thread 0's s_memtime cycles per phase
+// of the relaxation loop summed over edges (tools/sgd_stamps.py).
+#ifdef SLAM_SGD_STAMPS
+__device__ unsigned long long g_sgd_stamps[8];
+#define SGD_STAMP(q)                                                    \
+    do {                                                                \
+        if (threadIdx.x == 0) {                                         \
+            const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+            acc_[q] += t1_ - t0_;                                       \
+            t0_ = t1_;                                                  \
+        }                                                               \
+    } while (0)
+#else
+#define SGD_STAMP(q) \
+    do {             \
+    } while (0)
+#endif
+
+// Vector (vmcnt-counted) loads of uniform addresses: buffer loads through a
+// descriptor of the array (the compiler turns plain uniform loads of
+// read-only memory into scalar loads, which count on lgkmcnt).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vrsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ int vld_i(__amdgpu_buffer_rsrc_t r, int i) {
+    return static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(r, i * 4, 0, 0));
+}
+__device__ __forceinline__ double vld_d(__amdgpu_buffer_rsrc_t r, int i) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8, 0, 0);
+    return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(v[1]) << 32) | v[0]));
+}
+
+template <bool IN_LDS, int BR>
+__global__ __launch_bounds__(relax_threads<IN_LDS>()) void sgd_relax_kernel(
+    double* __restrict__ g_poses, int32_t N, const int32_t* A, const int32_t* B, const double* TF,
+    const double* RT, const int32_t* __restrict__ Kp, const double* C, const double* __restrict__ gamma, double lr,
+    double sigma, int32_t sh) {
+    // The prefetch of A, B, TF and C goes through vld (vector loads counted by
+    // vmcnt): as scalar loads (uniform addresses) they shared lgkmcnt with the
+    // LDS traffic, so every LDS wait of an edge also waited for the next
+    // edges' prefetch from memory.
+    constexpr int kRelaxThreads = relax_threads<IN_LDS>();
+    constexpr bool kOneWave = kRelaxThreads == 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nblk = ((N - 1) >> sh) + 1;
     double* off = reinterpret_cast<double*>(smem);                // [nblk][3] lazy offsets
@@ -355,44 +389,93 @@ __global__ __launch_bounds__(kRelaxThreads) void sgd_relax_kernel(
         alpha[j] = 1.0 / gamma[j];
         alpha[j] *= lr;
     }
-    const M3 S = diag3(sigma);
+    const double w2 = 2.0 / sigma;
 
-    // explicit node of thread tid for edge (a, b): the remainder of a's block,
-    // then b's block (when different); -1 when the thread has none
-    auto explicit_node = [&](int a, int b) {
+    // explicit node t (a thread slot) of edge (a, b): the remainder of a's
+    // block, then b's block (when different); -1 past them
+    auto node_of = [&](int a, int b, int t) {
         const int ba = a >> sh, bb = b >> sh;
         const int n1 = min(N, (ba + 1) << sh) - (a + 1);
         const int n2 = bb > ba ? min(N, (bb + 1) << sh) - (bb << sh) : 0;
-        return tid < n1 ? a + 1 + tid : (tid < n1 + n2 ? (bb << sh) + (tid - n1) : -1);
+        return t < n1 ? a + 1 + t : (t < n1 + n2 ? (bb << sh) + (t - n1) : -1);
     };
-    // Edge k's pose-independent operands are loaded during edge k-1.
-    struct Pre {
-        int a, b, ni;
-        double z[9], ca[3], cb[3], ci[3], irtw[3];
+    // Operands in three stages so that no load sits on the per-edge chain:
+    // (a, b) of edge k + 2 are loaded during edge k; edge k + 1's transform and
+    // C values (which need its a and b) are issued during edge k; edge k uses
+    // what arrived meanwhile.
+    const auto rA = vrsrc(A), rB = vrsrc(B), rTF = vrsrc(TF), rRT = vrsrc(RT), rC = vrsrc(C);
+    struct Ops {
+        int a, b, ni[kRelaxSlots];
+        double z[9], ca[3], cb[3], irtw[3], ci[kRelaxSlots][3];
     };
-    auto fetch = [&](int k, Pre& q) {
-        q.a = A[k];
-        q.b = B[k];
+    auto issue = [&](int k, int a, int b, Ops& q) {
+        q.a = a;
+        q.b = b;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) q.z[t] = TF[9 * static_cast<int64_t>(k) + t];
-        q.ni = explicit_node(q.a, q.b);
-        const int i0 = q.ni >= 0 ? q.ni : q.a;
+        for (int t = 0; t < 9; ++t) q.z[t] = vld_d(rTF, 9 * k + t);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            q.ca[j] = C[3 * (q.a + 1) + j];
-            q.cb[j] = C[3 * (q.b + 1) + j];
-            q.ci[j] = C[3 * (i0 + 1) + j];
-            q.irtw[j] = 1.0 / (q.cb[j] - q.ca[j]);   // pose-independent: off the dependent chain
+            q.ca[j] = vld_d(rC, 3 * (a + 1) + j);
+            q.cb[j] = vld_d(rC, 3 * (b + 1) + j);
+            q.irtw[j] = vld_d(rRT, 3 * k + j);
+        }
+#pragma unroll
+        for (int u = 0; u < kRelaxSlots; ++u) {
+            q.ni[u] = node_of(a, b, tid + u * kRelaxThreads);
+            const int i0 = q.ni[u] >= 0 ? q.ni[u] : a;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) q.ci[u][j] = vld_d(rC, 3 * (i0 + 1) + j);
         }
     };
-    Pre cur, nxt;
-    if (K > 0) fetch(0, cur);
+    Ops cur, nxt;
+    int an = 0, bn = 0;   // edge k + 1's (a, b)
+    if (K > 0) {
+        issue(0, A[0], B[0], cur);
+        an = A[min(1, K - 1)];
+        bn = B[min(1, K - 1)];
+    }
+#ifdef SLAM_SGD_STAMPS
+    unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+    unsigned long long acc_[6] = {0, 0, 0, 0, 0, 0};
+#endif
     for (int k = 0; k < K; ++k) {
-        if (k + 1 < K) fetch(k + 1, nxt);
+        // unconditional loads (indices clamped at the last edge): the compiler
+        // then knows how many loads are younger than each operand and waits
+        // only for that one, not for everything just issued (vmcnt(0))
+        const int k2 = min(k + 2, K - 1);
+        const int a2 = vld_i(rA, k2), b2 = vld_i(rB, k2);   // made uniform at the end of the edge
+        issue(min(k + 1, K - 1), an, bn, nxt);
         const int a = cur.a, b = cur.b;
+        const double(&irtw)[3] = cur.irtw;   // 1 / (C[b+1] - C[a+1]): sgd_irtw_kernel
+        SGD_STAMP(0);
+
+        const int ba = a >> sh, bb = b >> sh;
+        // one wave: the reads of this edge's updates go out with the residual's
+        // (nothing writes them before the updates below), so their latency hides
+        // under the residual chain: a's block remainder and b's block (<=
+        // kRelaxSlots nodes per lane; 2^(sh+1) = 128 = kRelaxSlots x 64 for
+        // LDS-resident graphs), whole blocks (ba, nblk) in BR rounds
+        double pv[kRelaxSlots][3], ov[BR][3], cv[BR][3];
+        if constexpr (kOneWave) {
+#pragma unroll
+            for (int u = 0; u < kRelaxSlots; ++u) {
+                const int i = cur.ni[u] >= 0 ? cur.ni[u] : a;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) pv[u][j] = P[3 * i + j];
+            }
+#pragma unroll
+            for (int r = 0; r < BR; ++r) {
+                const int q = ba + 1 + tid + r * kRelaxThreads;
+                const int qc = q < nblk ? q : ba;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    ov[r][j] = off[3 * qc + j];
+                    cv[r][j] = cA[3 * qc + j];
+                }
+            }
+        }
 
         // ---- residual (src/pose_graph_optimization.py:29-34), uniform -----------
-        const int ba = a >> sh, bb = b >> sh;
         double pa[3], pb[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -411,76 +494,118 @@ __global__ __launch_bounds__(kRelaxThreads) void sgd_relax_kernel(
         r[0] = Pb.a[0][2] - pb[0];
         r[1] = Pb.a[1][2] - pb[1];
         r[2] = py_mod_2pi(atan2(Pb.a[1][0], Pb.a[0][0]) - pb[2]);
-        const M3 Wi = m3_inv_adj(m3_mul(m3_mul(m3_transpose(R), S), R));
+        // d = 2 inv(R^T sigma I R) r = (2 / sigma) r: R is a rotation, so the
+        // inverse is I / sigma exactly; the reference's LAPACK inverse of the
+        // rounded product differs from it in the last bits only (and beta is
+        // clamped to r whenever 2 (b - a) lr > 1, e.g. always at lr = 1)
         double beta[3];
         const int L = b - a;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const M3& w = Wi;
-            const double dj = fma(2.0 * w.a[j][2], r[2], fma(2.0 * w.a[j][1], r[1], (2.0 * w.a[j][0]) * r[0]));
+            const double dj = w2 * r[j];
             double bj = (static_cast<double>(L) * dj) * alpha[j];
             if (fabs(bj) > fabs(r[j])) bj = r[j];
             beta[j] = bj;
         }
-        // Every thread read P[a] and P[b] above, and node b is one of this
-        // edge's explicit nodes: its owner may not write it before every wave
-        // has read it.  Each wave counts itself in after its residual chain
-        // (which consumed the reads); only the owner of b waits for the count
-        // (normally already complete), the other threads go on.  Release (every
-        // lane's reads of P ordered before the count) / acquire (the owner's
-        // write of P[b] ordered after it), workgroup scope; with P in LDS the
-        // fence covers LDS only (it does not wait for the next edge's
-        // prefetched global operands)
-        if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if ((tid & 63) == 0) __hip_atomic_fetch_add(&rd_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        SGD_STAMP(1);
+        // Several waves: every thread read P[a] and P[b] above, and node b is
+        // one of this edge's explicit nodes, so its owner may not write it
+        // before every wave has read it.  Each wave counts itself in after its
+        // residual chain (which consumed the reads); only the owner of b waits
+        // for the count (normally already complete).  Release (every lane's
+        // reads of P before the count) / acquire (the owner's write of P[b]
+        // after it), workgroup scope; with P in LDS the fence covers LDS only.
+        // One wave: LDS operations of a wave complete in order, nothing to do.
+        if constexpr (!kOneWave) {
+            if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if ((tid & 63) == 0) __hip_atomic_fetch_add(&rd_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         const uint32_t rd_target = static_cast<uint32_t>(kRelaxThreads / 64) * static_cast<uint32_t>(k + 1);
-        // ---- explicit nodes (a's block remainder, b's block) ----------------------
-        {
-            int i = cur.ni;
-            int t = tid;
-            double cij[3] = {cur.ci[0], cur.ci[1], cur.ci[2]};
-            while (i >= 0) {
-                if (i == b) {
-                    while (__hip_atomic_load(&rd_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < rd_target)
-                        __builtin_amdgcn_s_sleep(1);
-                    if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        SGD_STAMP(2);
+        if constexpr (kOneWave) {
+            // ---- one wave: the writes of the values read above ----------------------
+            SGD_STAMP(3);
+#pragma unroll
+            for (int u = 0; u < kRelaxSlots; ++u) {
+                const int i = cur.ni[u];
+                if (i >= 0) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j)
+                        P[3 * i + j] = pv[u][j] + (i <= b ? beta[j] * ((cur.ci[u][j] - cur.ca[j]) * irtw[j]) : beta[j]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < BR; ++r) {
+                const int q = ba + 1 + tid + r * kRelaxThreads;
+                if (q < bb) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const double g = beta[j] * irtw[j];
+                        cA[3 * q + j] = cv[r][j] + g;
+                        off[3 * q + j] = ov[r][j] - g * cur.ca[j];
+                    }
+                } else if (q > bb && q < nblk) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) off[3 * q + j] = ov[r][j] + beta[j];
+                }
+            }
+        } else {
+            // ---- explicit nodes (a's block remainder, b's block) ----------------------
+            auto move = [&](int i, const double (&ci)[3]) {
+                if constexpr (!kOneWave) {
+                    if (i == b) {
+                        while (__hip_atomic_load(&rd_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < rd_target)
+                            __builtin_amdgcn_s_sleep(1);
+                        if constexpr (IN_LDS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    }
                 }
                 if (i <= b) {
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((cij[j] - cur.ca[j]) * cur.irtw[j]);
+                    for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j] * ((ci[j] - cur.ca[j]) * irtw[j]);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 3; ++j) P[3 * i + j] += beta[j];
                 }
-                t += kRelaxThreads;   // more than one explicit node per thread only when 2^(sh+1) > block
-                if (t >= 2 * bs) break;
-                const int n1 = min(N, (ba + 1) << sh) - (a + 1);
-                const int n2 = bb > ba ? min(N, (bb + 1) << sh) - (bb << sh) : 0;
-                i = t < n1 ? a + 1 + t : (t < n1 + n2 ? (bb << sh) + (t - n1) : -1);
-                if (i >= 0)
+            };
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) cij[j] = C[3 * (i + 1) + j];
+            for (int u = 0; u < kRelaxSlots; ++u)
+                if (cur.ni[u] >= 0) move(cur.ni[u], cur.ci[u]);
+            // more explicit nodes than prefetched slots only when 2^(sh+1) > kRelaxSlots * threads
+            for (int t = tid + kRelaxSlots * kRelaxThreads; t < 2 * bs; t += kRelaxThreads) {
+                const int i = node_of(a, b, t);
+                if (i < 0) break;
+                const double ci[3] = {C[3 * (i + 1)], C[3 * (i + 1) + 1], C[3 * (i + 1) + 2]};
+                move(i, ci);
             }
-        }
-        // ---- whole blocks: ramp (ba, bb) as C coefficients, tail (bb, nblk) --------
-        for (int q = ba + 1 + tid; q < nblk; q += kRelaxThreads) {
-            if (q < bb) {
+            SGD_STAMP(3);
+            // ---- whole blocks: ramp (ba, bb) as C coefficients, tail (bb, nblk) --------
+            for (int q = ba + 1 + tid; q < nblk; q += kRelaxThreads) {
+                if (q < bb) {
 #pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const double g = beta[j] * cur.irtw[j];
-                    cA[3 * q + j] += g;
-                    off[3 * q + j] -= g * cur.ca[j];
+                    for (int j = 0; j < 3; ++j) {
+                        const double g = beta[j] * irtw[j];
+                        cA[3 * q + j] += g;
+                        off[3 * q + j] -= g * cur.ca[j];
+                    }
+                } else if (q > bb) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) off[3 * q + j] += beta[j];
                 }
-            } else if (q > bb) {
-#pragma unroll
-                for (int j = 0; j < 3; ++j) off[3 * q + j] += beta[j];
             }
         }
-        __syncthreads();
+        SGD_STAMP(4);
+        if constexpr (!kOneWave) __syncthreads();
+        SGD_STAMP(5);
         cur = nxt;
+        an = __builtin_amdgcn_readfirstlane(a2);
+        bn = __builtin_amdgcn_readfirstlane(b2);
     }
+#ifdef SLAM_SGD_STAMPS
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 6; ++q) g_sgd_stamps[q] += acc_[q];
+#endif
     // fold the lazy terms back
     for (int i = tid; i < N; i += kRelaxThreads) {
         const int q = i >> sh;
@@ -530,10 +655,26 @@ using namespace slamhip;
 
 extern "C" {
 
+// Diagnostics: copy (and clear) the relaxation's phase cycles; SLAM_EINVAL
+// unless built with -DSLAM_SGD_STAMPS.
+int slam_pgo_sgd_stamps(unsigned long long* out8) {
+#ifdef SLAM_SGD_STAMPS
+    if (!out8) return fail(SLAM_EINVAL, "sgd stamps: null");
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_sgd_stamps), 8 * sizeof(unsigned long long));
+    unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sgd_stamps), z, sizeof(z));
+    return ok();
+#else
+    (void)out8;
+    return fail(SLAM_EINVAL, "sgd stamps: built without SLAM_SGD_STAMPS");
+#endif
+}
+
 int64_t slam_pgo_sgd_work_size(int32_t N, int32_t E) {
-    // doubles: invM (3N) | dw (3E) | gamma (4) | C (3N+3) | TF (9E) | then int32: A, B, IDX (E each) | K
+    // doubles: invM (3N) | dw (3E) | gamma (4) | C (3N+3) | TF (9E) | RT (3E) | then int32: A, B, IDX (E each) | K
     return 3 * static_cast<int64_t>(N) + 3 * static_cast<int64_t>(E) + 4 + 3 * (static_cast<int64_t>(N) + 1) +
-           9 * static_cast<int64_t>(E) + (3 * static_cast<int64_t>(E) + 2) / 2;
+           12 * static_cast<int64_t>(E) + (3 * static_cast<int64_t>(E) + 2) / 2;
 }
 
 int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb,
@@ -548,7 +689,8 @@ int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int
     double* gamma = dw + 3 * static_cast<int64_t>(E);
     double* C = gamma + 4;
     double* TF = C + 3 * (static_cast<int64_t>(N) + 1);
-    int32_t* A = reinterpret_cast<int32_t*>(TF + 9 * static_cast<int64_t>(E));
+    double* RT = TF + 9 * static_cast<int64_t>(E);
+    int32_t* A = reinterpret_cast<int32_t*>(RT + 3 * static_cast<int64_t>(E));
     int32_t* Bv = A + E;
     int32_t* IDX = Bv + E;
     int32_t* Kp = IDX + E;
@@ -559,22 +701,28 @@ int slam_pgo_sgd_step_f64(double* poses, int32_t N, const int32_t* ea, const int
     hipLaunchKernelGGL(sgd_weights_kernel, dim3((N + 127) / 128), dim3(128), 0, s, N, A, Bv, IDX, Kp, dw,
                        invM);
     hipLaunchKernelGGL(sgd_prefix_kernel, dim3(1), dim3(kRelaxBlock), 0, s, invM, N, C);
+    hipLaunchKernelGGL(sgd_irtw_kernel, dim3((E + 255) / 256), dim3(256), 0, s, A, Bv, Kp, C, E, RT);
     // lazy-offset block size 2^sh: >= 64 nodes, at most kMaxOffBlocks blocks
     int sh = 6;
     while ((((N - 1) >> sh) + 1) > kMaxOffBlocks) ++sh;
     const size_t offb = 2 * 3 * static_cast<size_t>(((N - 1) >> sh) + 1) * sizeof(double);   // off + cA
     if (N <= kLdsPoses) {
+        // one wave; whole-block updates in BR rounds of 64 (nblk <= 96 here)
         const size_t lds = offb + 3 * static_cast<size_t>(N) * sizeof(double);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        hipLaunchKernelGGL(sgd_relax_kernel<true>, dim3(1), dim3(kRelaxThreads), lds, s, poses, N, A, Bv, TF,
-                           Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
+        const int nblk = ((N - 1) >> sh) + 1;
+        auto kern = nblk <= 64 ? sgd_relax_kernel<true, 1> : sgd_relax_kernel<true, 2>;
+        static_assert(((kLdsPoses - 1) >> 6) + 1 <= 2 * 64, "BR = 2 covers every LDS-resident graph");
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds));
+        hipLaunchKernelGGL(kern, dim3(1), dim3(relax_threads<true>()), lds, s, poses, N, A, Bv, TF, RT, Kp, C,
+                           gamma, learning_rate, loop_closure_uncertainty, sh);
     } else {
         // off + cA reach 2 x 3 x 2048 doubles (96 KiB): above the 64 KiB default
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(sgd_relax_kernel<false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(offb));
-        hipLaunchKernelGGL(sgd_relax_kernel<false>, dim3(1), dim3(kRelaxThreads), offb, s, poses, N, A, Bv,
-                           TF, Kp, C, gamma, learning_rate, loop_closure_uncertainty, sh);
+        auto kern = sgd_relax_kernel<false, 1>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(offb));
+        hipLaunchKernelGGL(kern, dim3(1), dim3(relax_threads<false>()), offb, s, poses, N, A, Bv, TF, RT, Kp, C,
+                           gamma, learning_rate, loop_closure_uncertainty, sh);
     }
     return check_launch("pgo sgd kernels");
 }

@@ -387,10 +387,11 @@ def test_default_schedule_large_batch(k):
 
 def test_gangs_are_bit_identical(k):
     """Gangs (a pair's 64-query groups dealt over 2..17 workgroups that
-    exchange their exact partial sums every iteration) return the single
-    launch's transforms, errors, iteration counts and histories bit for bit:
-    every part count, every pair a gang (64 of 64 heads), and the default
-    tiers (8 gangs beside 56 CU-exclusive heads)."""
+    exchange their exact partial sums every iteration) and teams (parts = 0:
+    one workgroup per query group, the group's search split over its 4 waves)
+    return the single launch's transforms, errors, iteration counts and
+    histories bit for bit: every part count, every pair a gang (64 of 64
+    heads), and the tiers with CU-exclusive heads beside them."""
     from slamhip import _abi
     lib = _abi.lib()
     n = 1100
@@ -401,7 +402,7 @@ def test_gangs_are_bit_identical(k):
         single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
         assert lib.slam_icp_set_schedule(4, 1024) == 0
         runs = {}
-        for gangs, parts in ((8, 4), (64, 2), (64, 3), (64, 5), (64, 9), (64, 17), (1, 4)):
+        for gangs, parts in ((8, 4), (64, 2), (64, 3), (64, 5), (64, 9), (64, 17), (1, 4), (64, 0), (8, 0)):
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
             runs[(gangs, parts)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() == 0

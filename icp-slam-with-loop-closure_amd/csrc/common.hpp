@@ -53,7 +53,11 @@ __device__ __forceinline__ SE2 load_se2(const double* p) {
 __device__ __forceinline__ void store_se2(double* p, const SE2& t) {
     p[0] = t.m00; p[1] = t.m01; p[2] = t.m02;
     p[3] = t.m10; p[4] = t.m11; p[5] = t.m12;
-    p[6] = 0.0;   p[7] = 0.0;   p[8] = 1.0;
+    // the constant row from registers set here: as a hoisted constant the
+    // zero pair was the ICP kernel's only VGPR spill
+    double z = 0.0, one = 1.0;
+    asm volatile("" : "+v"(z), "+v"(one));
+    p[6] = z;     p[7] = z;     p[8] = one;
 }
 
 // A @ B for SE(2) matrices with NumPy/OpenBLAS dgemm rounding: every entry is

@@ -215,9 +215,12 @@ int slam_icp_set_schedule_heads(int heads);
 /* The first `gangs` of those head pairs run as gangs of `parts` workgroups
  * (2..17) each: a pair's 64-query groups are dealt over the parts, which sit on
  * one XCD, hold one CU each, and exchange their exact partial sums every
- * iteration through a stream-ordered workspace (agent-scope write-through
- * stores and counter).  Results are bit-identical to the one-workgroup
- * kernels.  gangs = 0: off; defaults (24, 4). */
+ * iteration through a stream-ordered workspace (data-tagged 8-byte granules,
+ * agent-scope write-through stores, bounded polling).  parts = 0: teams, one
+ * workgroup per 64-query group (pairs up to 2,048 points), the group's search
+ * split over the workgroup's four waves (latency mode).  Results are
+ * bit-identical to the one-workgroup kernels.  gangs = 0: off; defaults
+ * (24, 4).  SLAM_EINVAL for gangs < 0, parts 1, < 0 or > 17. */
 int slam_icp_set_schedule_gangs(int gangs, int parts);
 /* Nonzero if a gang's workgroups ever failed to meet (a partner not resident
  * for ~seconds; the launch then ended without valid results).  slam_icp_status

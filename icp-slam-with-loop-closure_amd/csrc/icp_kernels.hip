@@ -277,6 +277,18 @@ constexpr int kWpe = 4;          // waves/SIMD the default 1081-point instance i
 // Screened distances are non-negative (or +inf), so their IEEE bit patterns
 // order like unsigned integers: the updates run on the bits (integer min /
 // med3 need no NaN canonicalisation of the loop-carried M1, M2).
+// Packed-key top-2 of the window scan (nn_window_pruned): K1 <= K2 the two
+// smallest keys seen.
+constexpr int kWinBits = 5;   // kWin * kSub = 32 window offsets
+constexpr uint32_t kWinLow = (1u << kWinBits) - 1;
+static_assert(kWin * kSub == 1 << kWinBits, "window offsets fill the key's low bits");
+__device__ __forceinline__ void take_key(uint32_t key, uint32_t& K1, uint32_t& K2) {
+    uint32_t md;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(md) : "v"(K1), "v"(K2), "v"(key));
+    K2 = md;
+    K1 = min(K1, key);
+}
+
 __device__ __forceinline__ void take_cand(float d, int j, float& M1, float& M2, int& J1) {
     const uint32_t db = __float_as_uint(d), m1 = __float_as_uint(M1), m2 = __float_as_uint(M2);
     J1 = db < m1 ? j : J1;
@@ -330,19 +342,41 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         const int lo = (kWin & 1) ? kWin / 2 : kWin / 2 - ((pred[k] & (kSub - 1)) >= kSub / 2 ? 1 : 0);
         ws[k] = min(max((pred[k] >> 3) - lo, 0), nsub - kWin);
     }
-    // 1. windows (J1 holds the offset inside the window until the end of the loop)
+    // 1. windows, as a top-2 of packed keys: a candidate's screened distance bits
+    //    with the low kWinBits replaced by its offset in the window, so that one
+    //    v_and_or + v_min + v_med3 per candidate keep the two smallest keys and
+    //    the winner's offset (ties: the earlier offset, as take_cand).  A key
+    //    sits within 2^kWinBits ulps below its distance.  Unpacked afterwards:
+    //    M1 = the winner's key truncated (<= its distance), M2 = the runner-up
+    //    key with the low bits set (>= the runner-up's distance: every test that
+    //    needs M2 from above — settling, group mask, visits — stays valid), and
+    //    the certification reads M2 truncated (<= the true runner-up); keys
+    //    that differ only in the dropped bits are then never certified apart,
+    //    so a near-tie inside the window takes the exact fallback
+    uint32_t K1[QPT], K2[QPT];
+#pragma unroll
+    for (int k = 0; k < QPT; ++k) {
+        K1[k] = 0xffffffffu;
+        K2[k] = 0xffffffffu;
+    }
 #pragma unroll 2
     for (int t = 0; t < kWin * kSub; t += 2) {
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
             const float4 pp = *reinterpret_cast<const float4*>(candf + ws[k] * kSub + t);
             const f32x2v d = screen_pair(pp, qx[k], qy[k]);
-            take_cand(d.x, t, M1[k], M2[k], J1[k]);
-            take_cand(d.y, t + 1, M1[k], M2[k], J1[k]);
+            take_key((__float_as_uint(d.x) & ~kWinLow) | static_cast<uint32_t>(t), K1[k], K2[k]);
+            take_key((__float_as_uint(d.y) & ~kWinLow) | static_cast<uint32_t>(t + 1), K1[k], K2[k]);
         }
     }
 #pragma unroll
-    for (int k = 0; k < QPT; ++k) J1[k] += ws[k] * kSub;
+    for (int k = 0; k < QPT; ++k) {
+        if (k < NQ) {
+            J1[k] = static_cast<int>(K1[k] & kWinLow) + ws[k] * kSub;
+            M1[k] = __uint_as_float(K1[k] & ~kWinLow);
+            M2[k] = __uint_as_float(min(K2[k] | kWinLow, 0x7f800000u));   // capped at +inf
+        }
+    }
     if (counting) {
 #pragma unroll
         for (int k = 0; k < QPT; ++k) nev += kWin * kSub * __popcll(__ballot(valid[k]));
@@ -972,7 +1006,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     } else if (i < n1 && n2 > 1) {
                         const double2 c = PRUNE ? cw[k] : cand[j1];
                         const double d1 = exact_d2(c.x, c.y, qx[k], qy[k]);
-                        const double s2 = static_cast<double>(fminf(M2[k], b2));   // every other j: d32 >= s2
+                        // every other j: d32 >= s2 (PRUNE: M2 may still hold the window's
+                        // runner-up key rounded up, so its truncation is the bound)
+                        const double s2 = PRUNE ? static_cast<double>(__uint_as_float(__float_as_uint(M2[k]) & ~kWinLow))
+                                                : static_cast<double>(fminf(M2[k], b2));
                         const double cq = fmax(fabs(qx[k]), fabs(qy[k]));
                         const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (cmax + cq);
 #ifdef SLAM_ABL_CERT

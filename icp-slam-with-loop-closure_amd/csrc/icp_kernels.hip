@@ -85,6 +85,10 @@ struct IcpArgs {
     uint64_t* gang_slots;    // [n_gangs][2][gang][32] tagged granules, zeroed before the launch
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
+#ifndef SLAM_TAIL_SHARE
+#define SLAM_TAIL_SHARE 1
+#endif
+constexpr size_t kTailShare = SLAM_TAIL_SHARE;   // gang / team workgroups per CU (LDS requested: kMaxLds / share)
 constexpr int kGangSweep = 32;        // parts an exchange sweep covers (16 loads per lane)
 constexpr uint32_t kGangSpinLimit = 1u << 26;   // ~seconds of polling: a lost partner ends the launch
 __device__ int g_gang_timeout;        // set when a gang partner never arrived
@@ -1932,9 +1936,10 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
                                 static_cast<size_t>(a.cand_cap) * (sizeof(double2) + sizeof(float2)) +
                                 static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) + team_xbuf_words() * sizeof(uint32_t);
         if (lds_need > kMaxLds) return fail(SLAM_EINVAL, "icp teams: LDS");
+        const size_t lds = max(lds_need, kMaxLds / kTailShare);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(icp_team_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kMaxLds));
-        hipLaunchKernelGGL(icp_team_kernel, dim3((G + 7) / 8 * 8 * parts), dim3(kTeamBlock), kMaxLds, s, a);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        hipLaunchKernelGGL(icp_team_kernel, dim3((G + 7) / 8 * 8 * parts), dim3(kTeamBlock), lds, s, a);
         return check_launch("icp team kernel");
     }
     const GangInstance* gi = pick_gang_instance(max_n1, parts);
@@ -1951,7 +1956,7 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
                             static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
                             static_cast<size_t>(gi->block) * 2 * sizeof(int32_t);
     if (lds_need > kMaxLds) return fail(SLAM_EINVAL, "icp gangs: LDS");
-    const size_t lds = kMaxLds;   // whole CU: a gang's latency is its slowest part
+    const size_t lds = max(lds_need, kMaxLds / kTailShare);   // 1: whole CU (a gang's latency is its slowest part)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gi->fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds));
     const int blocks = (G + 7) / 8 * 8 * parts;

@@ -9,15 +9,18 @@
 //                      sequential sum), W_e = inv(R sigma R^T); gamma = the
 //                      first minimum-norm diag(W_e) (sgd_gamma_kernel).
 //     pass 2 (:27-49)  sgd_prefix_kernel: prefix sums C of 1/M (pose-independent
-//                      within a step); sgd_relax_kernel: ONE persistent workgroup
-//                      walks the loop edges in networkx order (each edge reads
-//                      poses the previous edges moved — a true sequential
-//                      dependency), ramps (a, b] by C differences and moves the
-//                      tail i > b by beta through lazy per-block offsets.
+//                      within a step), sgd_irtw_kernel: 1 / (C[b+1] - C[a+1]) per
+//                      edge; sgd_relax_kernel: ONE persistent wave (poses in
+//                      LDS; a 256-thread workgroup when they are not) walks the
+//                      loop edges in networkx order (each edge reads poses the
+//                      previous edges moved — a true sequential dependency),
+//                      ramps (a, b] by C differences and moves the tail i > b by
+//                      beta through lazy per-block offsets.
 //   recompute_pose_graph_orientation (:51-57)  orient_kernel.
 //
-// Rounding: the per-edge residual, d = 2 inv(R^T sigma R) r and the clamp are
-// evaluated like the reference; the ramp uses prefix-sum differences and the
+// Rounding: the per-edge residual and the clamp are evaluated like the
+// reference, d = 2 inv(R^T sigma R) r as (2 / sigma) r (exact for a rotation R;
+// the reference's LAPACK inverse differs in the last bits); the ramp uses prefix-sum differences and the
 // tail shifts are summed per block instead of the reference's left-to-right
 // running sums, so poses agree to rounding (tests: 1e-9 on positions after 20
 // steps of the reference's lap graph).

@@ -902,6 +902,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         asm volatile("" : "+v"(tid));
         double qx[QPT], qy[QPT];
         int bi[QPT];
+        double dq[QPT];   // exact squared distance to the match (the error term of the sums)
         if constexpr (SCREEN) {
             // ---- fp32 screen over LDS-resident candidates ---------------------
             {
@@ -1005,11 +1006,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     j1 = min(j1, n2 - 1);
                     bi[k] = j1;
                     bool ok = true;
+                    const double2 c = PRUNE ? cw[k] : cand[j1];
+                    const double d1 = exact_d2(c.x, c.y, qx[k], qy[k]);
+                    dq[k] = d1;   // = the sums' (pc1_t - pc2[corr])**2 bit for bit (same operands)
                     if (!screen) {
                         ok = i >= n1;   // |coordinates| >= 1e18: every query takes the exact path
                     } else if (i < n1 && n2 > 1) {
-                        const double2 c = PRUNE ? cw[k] : cand[j1];
-                        const double d1 = exact_d2(c.x, c.y, qx[k], qy[k]);
                         // every other j: d32 >= s2 (PRUNE: M2 may still hold the window's
                         // runner-up key rounded up, so its truncation is the bound)
                         const double s2 = PRUNE ? static_cast<double>(__uint_as_float(__float_as_uint(M2[k]) & ~kWinLow))
@@ -1051,7 +1053,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                                 bj = oj;
                             }
                         }
-                        if (lane == src) bi[k] = bj;
+                        if (lane == src) {
+                            bi[k] = bj;
+                            dq[k] = bd;
+                        }
                     }
                 }
                 stamp(1);
@@ -1099,6 +1104,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     }
                 }
             }
+#pragma unroll
+            for (int k = 0; k < QPT; ++k) dq[k] = best[k];
         }
 
         // ---- src/icp.py:64,68 + 22-46  error, centroids, cross-covariance ------
@@ -1112,8 +1119,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         // (q - mu_q = R_T (p - mu_p) and sum (m - pc2_avg) = 0).
         double tot;
         {
-            // the query point is recomputed from a re-read pc1 row (bit-identical
-            // to qx, qy) so those need not stay live through the sums
+            // the pc1 row is re-read (the untransformed point of the (p - c) m^T
+            // terms); the error term is the match's exact distance kept from the
+            // search (dq), so the query point need not stay live or be recomputed
             int tr = threadIdx.x;
             asm volatile("" : "+v"(tr));
             const double2 c = *reinterpret_cast<const double2*>(pconst + kPcX);
@@ -1133,11 +1141,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 if (i < n1) {
                     const double2 m = resident ? cand[bi[k]] : p2[bi[k]];
                     const double2 p = p1[i];
-                    const double x = fma(T.m02, 1.0, fma(T.m01, p.y, T.m00 * p.x));
-                    const double y = fma(T.m12, 1.0, fma(T.m11, p.y, T.m10 * p.x));
                     rsum_add(m.x, gm, acc[0], acc[1]);
                     rsum_add(m.y, gm, acc[2], acc[3]);
-                    rsum_add(exact_d2(m.x, m.y, x, y), gd, acc[4], acc[5]);   // (pc1_t - pc2[corr])**2
+                    rsum_add(dq[k], gd, acc[4], acc[5]);   // (pc1_t - pc2[corr])**2
                     const double ax = p.x - c.x, ay = p.y - c.y;
                     rsum_add(ax * m.x, gs, acc[6], acc[7]);
                     rsum_add(ax * m.y, gs, acc[8], acc[9]);

@@ -432,6 +432,9 @@ __global__ __launch_bounds__(relax_threads<IN_LDS>()) void sgd_relax_kernel(
     };
     Ops cur, nxt;
     int an = 0, bn = 0;   // edge k + 1's (a, b)
+    long long th_bits = 0;   // heading bits of the cached sin/cos (valid once th_set)
+    bool th_set = false;
+    double sn_c = 0.0, cs_c = 1.0;
     if (K > 0) {
         issue(0, A[0], B[0], cur);
         an = A[min(1, K - 1)];
@@ -485,7 +488,18 @@ __global__ __launch_bounds__(relax_threads<IN_LDS>()) void sgd_relax_kernel(
             pa[j] = P[3 * a + j] + off[3 * ba + j] + cA[3 * ba + j] * cur.ca[j];
             pb[j] = P[3 * b + j] + off[3 * bb + j] + cA[3 * bb + j] * cur.cb[j];
         }
-        const M3 R = rot_z(pa[2]);                // construct_R(pg, a)
+        // construct_R(pg, a): sin/cos cached across edges of the same heading
+        // bits (consecutive edges leaving one node: nothing moves node a between
+        // them), so the cached values are the ones sincos would return
+        if (!th_set || __double_as_longlong(pa[2]) != th_bits) {
+            sincos(pa[2], &sn_c, &cs_c);
+            th_bits = __double_as_longlong(pa[2]);
+            th_set = true;
+        }
+        M3 R;
+        R.a[0][0] = cs_c;  R.a[0][1] = -sn_c; R.a[0][2] = 0.0;
+        R.a[1][0] = sn_c;  R.a[1][1] = cs_c;  R.a[1][2] = 0.0;
+        R.a[2][0] = 0.0;   R.a[2][1] = 0.0;   R.a[2][2] = 1.0;
         M3 Pa = R;                                // utils.pose_to_mat(poses[a])
         Pa.a[0][2] = pa[0];
         Pa.a[1][2] = pa[1];

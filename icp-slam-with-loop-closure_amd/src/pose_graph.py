@@ -20,7 +20,14 @@ Gauss-Newton (``optimize_pose_graph``), which needs X_b = X_a z for every edge:
   and image loop closures, reference scripts/main.py:305,
   src/loop_closure_detection.py:141) or ``"relative"`` for X_j = X_i T (the
   proximity closures, which run ``icp(pc_j, pc_i)``, reference
-  src/loop_closure_detection.py:34).
+  src/loop_closure_detection.py:34);
+* ``constraint`` — set by every ``add_constraint`` call: the edge is a
+  measurement added after construction (so an (i, i+1) edge carrying it is
+  not a constructor delta, even without a convention).
+
+An edge with none of these keys (a graph built by the reference's own
+PoseGraph, a reference pickle, or a flipped graph) is classified per edge by
+its shape: (i, i+1) is a constructor delta at the current heading.
 """
 import pickle
 
@@ -61,6 +68,7 @@ class PoseGraph():
         self.graph.add_edge(i, j, object=transformation)
         attrs = self.graph.edges[i, j]
         attrs.pop("heading", None)
+        attrs["constraint"] = True
         if convention is None:
             attrs.pop("convention", None)
         else:
@@ -110,7 +118,12 @@ class PoseGraph():
 
         Cached: ``add_constraint`` / ``flip`` / ``load`` drop the cache, and
         a graph object or edge count changed behind the class's back does too
-        (scripts/main.py:325-326 runs the SGD step 50 times on one graph)."""
+        (scripts/main.py:325-326 runs the SGD step 50 times on one graph).
+        Edits that keep the edge count — ``graph.add_edge`` on an existing
+        edge, ``graph[a][b]["object"] = T``, or mutating a stored transform in
+        place — are NOT seen: make them through ``add_constraint`` or call
+        ``invalidate()`` afterwards (checking every edge's contents per call
+        would cost as much as the flattening the cache saves)."""
         n_edges = self.graph.number_of_edges()
         if self._flat is not None and self._flat[0] is self.graph and self._flat[1] == n_edges:
             return self._flat[2]
@@ -129,12 +142,21 @@ class PoseGraph():
         self._flat = (self.graph, n_edges, out)
         return out
 
+    def invalidate(self):
+        """Drop the flattened-edge cache (and the drop-in SGD solver keyed on
+        it) after editing ``graph`` directly."""
+        self._flat = None
+        self.__dict__.pop("_sgd_solver", None)
+
     def edge_kinds(self):
-        """Per edge in nx order: (heading or NaN, convention code) where the
-        code is 0 unknown, 1 "icp", 2 "relative"."""
+        """Per edge in nx order: (heading or NaN, convention code, added by
+        ``add_constraint``) where the code is 0 unknown, 1 "icp", 2
+        "relative"."""
         codes = {None: 0, "icp": 1, "relative": 2}
-        head, conv = [], []
+        head, conv, added = [], [], []
         for _, _, d in self.graph.edges(data=True):
             head.append(d.get("heading", np.nan))
             conv.append(codes.get(d.get("convention"), 0))
-        return np.asarray(head, dtype=np.float64), np.asarray(conv, dtype=np.int8)
+            added.append(bool(d.get("constraint", False)) or "convention" in d)
+        return (np.asarray(head, dtype=np.float64), np.asarray(conv, dtype=np.int8),
+                np.asarray(added, dtype=bool))

@@ -102,22 +102,25 @@ def gn_measurements(pose_graph, odometry_edges="global_delta", loop_edges="icp")
       ``convention="relative"`` (icp(pc_b, pc_a), ``detect_proximity``) is kept;
     * a constraint without a recorded convention follows ``loop_edges``.
 
-    A graph with no annotations at all (built by the reference's own
-    PoseGraph, or a reference pickle) falls back to the shape rule: (a, a+1)
-    edges are constructor deltas at the current pose's heading, the others
-    follow ``loop_edges``."""
+    An edge with no annotation at all (built by the reference's own
+    PoseGraph, loaded from a reference pickle, or flipped) is classified by
+    its shape, PER EDGE: (a, a+1) is a constructor delta at the current pose's
+    heading, any other edge follows ``loop_edges``.  So an unannotated pickle
+    that later gets closures added with a convention keeps its odometry
+    edges as deltas."""
     if odometry_edges not in ("global_delta", "relative") or loop_edges not in ("icp", "relative"):
         raise ValueError("odometry_edges in {global_delta, relative}, loop_edges in {icp, relative}")
     ea, eb, tf = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
     z = np.array(tf, dtype=np.float64).reshape(-1, 3, 3)
     if hasattr(pose_graph, "edge_kinds"):
-        head, conv = pose_graph.edge_kinds()
+        head, conv, added = pose_graph.edge_kinds()
     else:
-        head, conv = np.full(len(ea), np.nan), np.zeros(len(ea), np.int8)
+        head, conv, added = np.full(len(ea), np.nan), np.zeros(len(ea), np.int8), np.zeros(len(ea), bool)
     delta = ~np.isnan(head)
-    if not delta.any() and not conv.any():   # unannotated graph: the shape rule
-        delta = eb.astype(np.int64) == ea.astype(np.int64) + 1
-        head = np.where(delta, np.asarray(pose_graph.poses, dtype=np.float64)[ea, 2], np.nan)
+    bare = ~delta & ~added & (conv == 0) & (eb.astype(np.int64) == ea.astype(np.int64) + 1)
+    if bare.any():   # unannotated (a, a+1): the shape rule, at the current heading
+        head = np.where(bare, np.asarray(pose_graph.poses, dtype=np.float64)[ea, 2], head)
+        delta = delta | bare
     if odometry_edges == "global_delta" and delta.any():
         th = head[delta]
         c, s = np.cos(th), np.sin(th)

@@ -296,6 +296,61 @@ def test_gn_measurements_follow_recorded_conventions(tmp_path):
         pg.add_constraint(0, 5, np.eye(3), convention="global")
 
 
+def test_unannotated_pickle_plus_annotated_closures(tmp_path):
+    """A graph pickled without annotations (the reference's own PoseGraph, or
+    this repo before the annotations) that then gets closures added with a
+    convention (scripts/main_batched.py: load, then manual closures): the
+    shape rule is applied PER EDGE, so its (a, a+1) edges stay constructor
+    deltas and chi2 = 0 at the true poses.  A constraint added on an (a, a+1)
+    edge without a convention is NOT a delta (it follows loop_edges)."""
+    import pickle
+
+    import networkx as nx
+
+    import src.pose_graph as pgm
+    import src.pose_graph_optimization as pgo
+    from slamhip import se2, synthetic
+    s = synthetic.make_loop_sequence(400, seed=3, n_beams=31)
+    X = [se2.pose_to_mat(p) for p in s.truth]
+    g = nx.DiGraph()   # the reference's constructor (src/pose_graph.py:32-36): "object" only
+    g.add_edges_from((i, i + 1, {"object": se2.odom_change_to_mat(s.truth[i + 1] - s.truth[i])})
+                     for i in range(len(s.truth) - 1))
+    f = str(tmp_path / "ref.pickle")
+    with open(f, "wb") as fh:
+        pickle.dump((s.truth.copy(), g), fh)
+    q = pgm.PoseGraph(None)
+    q.load(f)
+    for a, b in s.loop_pairs:
+        a, b = int(a), int(b)
+        q.add_constraint(a, b, np.linalg.inv(X[b]) @ X[a], convention="icp")
+
+    def chi2(gr, **kw):
+        ea, eb, z = pgo.gn_measurements(gr, **kw)
+        return go.build_system(s.truth.copy(), ea.astype(np.int64), eb.astype(np.int64),
+                               go.edge_measurements(z), go.information(ea, eb))[3]
+    assert chi2(q) < 1e-20
+    # a convention-less constraint on (a, a+1): a relative measurement under loop_edges="relative"
+    q.add_constraint(10, 11, np.linalg.inv(X[10]) @ X[11])
+    assert chi2(q, loop_edges="relative") < 1e-20
+    assert chi2(q, loop_edges="icp") > 1e-8
+
+
+def test_edge_arrays_cache_invalidate():
+    """Edits that keep the edge count are not seen by the cache;
+    PoseGraph.invalidate() drops it (and the drop-in SGD solver keyed on it)."""
+    import src.pose_graph as pgm
+    poses = np.c_[np.arange(6.0), np.zeros(6), np.zeros(6)]
+    pg = pgm.PoseGraph(poses)
+    a = pg.edge_arrays()
+    pg.graph[1][2]["object"] = 2 * np.eye(3)
+    assert pg.edge_arrays() is a
+    pg._sgd_solver = ("stale", None)
+    pg.invalidate()
+    b = pg.edge_arrays()
+    assert b is not a and np.array_equal(b[2][1], 2 * np.eye(3))
+    assert not hasattr(pg, "_sgd_solver")
+
+
 def test_edge_arrays_cache_follows_the_graph():
     """PoseGraph.edge_arrays() is cached between SGD calls and rebuilt after
     add_constraint / flip / load or a direct change of the graph."""

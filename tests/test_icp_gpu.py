@@ -103,6 +103,36 @@ def test_batched_sequence_vs_oracle(k, oracle):
     assert np.abs(chain[:, :2] - seq.truth[:, :2] - (seq.odometry[0, :2] - seq.truth[0, :2])).max() < 0.5
 
 
+def _oracle_final_tf(pc1, pc2, init):
+    import icp_oracle
+    h, _ = icp_oracle.icp(homog(pc1), homog(pc2), init, 0.05, 100)
+    return h[-1], len(h) - 1
+
+
+def test_c2_full_sequence_chain_vs_oracle():
+    """Config C2 stand-in at full length (BASELINE.json configs[1], SURVEY.md
+    §8(d)): the 1,000-scan seed-1 sequence through scripts/main.py stage 1
+    (:236-256) — one batched launch on the GPU, the serial chain on the host —
+    against the reference flow (oracle ICP per pair on the host cores, the
+    same chain): every pair's iteration count equal, every chained pose within
+    the north star's 1e-5 (measured: ~1e-13)."""
+    import os
+    from joblib import Parallel, delayed
+    from slamhip import pipeline, se2, synthetic
+    n = 1000
+    seq = synthetic.make_sequence(n, seed=1)
+    r = pipeline.scan_matching(seq.odometry, seq.scans)
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    ref = Parallel(n_jobs=workers, backend="loky", batch_size=8)(
+        delayed(_oracle_final_tf)(seq.scans[i], seq.scans[i - 1], se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]))
+        for i in range(1, n))
+    assert np.array_equal(r.iters, np.array([it for _, it in ref]))
+    chain = se2.compose_chain(seq.odometry[0], np.stack([t for t, _ in ref]))
+    assert r.poses.shape == (n, 3)
+    assert np.abs(r.poses - chain).max() <= 1e-5
+    assert np.abs(r.tf - np.stack([t for t, _ in ref])).max() <= TOL
+
+
 def test_batch_is_order_independent_and_deterministic(k):
     n = 40
     seq, inits = _sequence_pairs(n, seed=7, n_beams=361)

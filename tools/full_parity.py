@@ -1,8 +1,16 @@
 """Parity of the benchmarked path over EVERY pair of the C3 stream: the GPU's
 batched ICP (default scheduler; the full 10k batch and the shards ranks 0 get
-at 2 / 4 / 8 GPUs, which run the CU-exclusive head pairs) against the CPU
-oracle (oracle/icp_oracle.py, vectorised NumPy, bit-exact with src/icp.py),
-run on the host cores with joblib.  GPU only; ~2 minutes on 16 cores.
+at 2 / 4 / 8 GPUs, which run the gang / CU-exclusive head tiers) against the
+CPU oracle (oracle/icp_oracle.py, vectorised NumPy, bit-exact with
+src/icp.py), run on the host cores with joblib.  GPU only; ~2 minutes on 16
+cores.
+
+Besides equality it records how close every stopping decision of the oracle
+run comes to its threshold (src/icp.py:86-94): per iteration k the margins
+|err_k - eps| and, from the second iteration, ||err_{k-1} - err_k| - thresh|;
+per pair the smallest of them, against the GPU-vs-oracle difference of the
+final error.  A margin below ~1e3 x that difference would mark a pair whose
+iteration count rides on rounding.
 
     python tools/full_parity.py [pairs] [workers] > profiles/rNN_full_parity.json
 """
@@ -20,11 +28,26 @@ os.environ.setdefault("OMP_NUM_THREADS", "1")
 from slamhip import se2, synthetic  # noqa: E402
 from slamhip import icp as k  # noqa: E402
 
+EPS, MAX_ITERS, THRESH = 0.05, 100, 1e-4
+
 
 def oracle_pair(pc1, pc2, init):
+    """icp_oracle.icp's loop (src/icp.py:72-97) keeping every iteration's error."""
     import icp_oracle
-    h, e = icp_oracle.icp(np.c_[pc1, np.ones(len(pc1))], np.c_[pc2, np.ones(len(pc2))], init, 0.05, 100)
-    return h[-1], float(e), len(h) - 1
+    a, b = np.c_[pc1, np.ones(len(pc1))], np.c_[pc2, np.ones(len(pc2))]
+    T, errs, it = init, [], 0
+    while True:
+        T, _, err = icp_oracle.icp_iteration(a, b, T)
+        errs.append(float(err))
+        if err < EPS or it > MAX_ITERS:
+            break
+        if len(errs) > 1 and abs(errs[-2] - err) < THRESH:
+            break
+        it += 1
+    e = np.array(errs)
+    m_eps = np.abs(e - EPS).min()
+    m_d = np.abs(np.abs(np.diff(e)) - THRESH).min() if len(e) > 1 else np.inf
+    return T, errs[-1], len(errs), float(m_eps), float(m_d)
 
 
 def main():
@@ -35,8 +58,11 @@ def main():
     ss = k.ScanSet(seq.scans)
     runs = {}
     for shard in (n, n // 2, n // 4, n // 8):
-        res = k.icp_batch(ss, np.arange(1, shard + 1), np.arange(0, shard), inits[:shard], epsilon=0.05, max_iters=100)
-        runs[shard] = res
+        runs[shard] = k.icp_batch(ss, np.arange(1, shard + 1), np.arange(0, shard), inits[:shard],
+                                  epsilon=EPS, max_iters=MAX_ITERS)
+    for shard in (n // 2, n // 4, n // 8):   # the last shard of each world size as well
+        runs[f"last_{shard}"] = (n - shard, k.icp_batch(ss, np.arange(n - shard + 1, n + 1), np.arange(n - shard, n),
+                                                         inits[n - shard:], epsilon=EPS, max_iters=MAX_ITERS))
     from joblib import Parallel, delayed
     t0 = time.perf_counter()
     ref = Parallel(n_jobs=workers, backend="loky", batch_size=16)(
@@ -45,17 +71,37 @@ def main():
     rtf = np.stack([r[0] for r in ref])
     rerr = np.array([r[1] for r in ref])
     rit = np.array([r[2] for r in ref])
+    m_eps = np.array([r[3] for r in ref])
+    m_d = np.array([r[4] for r in ref])
     out = {"workload": f"C3 stream seed 2025, {n} consecutive pairs of 1081-point scans, scripts/main.py parameters",
            "oracle": "oracle/icp_oracle.py (vectorised, bit-exact with the reference's src/icp.py)",
            "oracle_seconds": round(dt, 1), "oracle_workers": workers, "runs": {}}
-    for shard, res in runs.items():
-        dtf = np.abs(res.tf - rtf[:shard]).max(axis=(1, 2))
-        derr = np.abs(res.err - rerr[:shard]) / np.maximum(1.0, np.abs(rerr[:shard]))
-        out["runs"][f"first_{shard}_pairs"] = {
-            "pairs": shard, "iters_equal": int(np.sum(res.iters == rit[:shard])),
+    for key, val in runs.items():
+        lo, res = (0, val) if isinstance(key, int) else val
+        cnt = len(res.iters)
+        sl = slice(lo, lo + cnt)
+        dtf = np.abs(res.tf - rtf[sl]).max(axis=(1, 2))
+        derr = np.abs(res.err - rerr[sl]) / np.maximum(1.0, np.abs(rerr[sl]))
+        name = f"first_{key}_pairs" if isinstance(key, int) else f"last_{key[5:]}_pairs"
+        out["runs"][name] = {
+            "pairs": cnt, "first_pair": lo, "iters_equal": int(np.sum(res.iters == rit[sl])),
             "max_abs_tf_diff": float(dtf.max()), "max_rel_err_diff": float(derr.max()),
-            "pairs_over_1e-9": int(np.sum((dtf > 1e-9) | (derr > 1e-9) | (res.iters != rit[:shard]))),
+            "pairs_over_1e-9": int(np.sum((dtf > 1e-9) | (derr > 1e-9) | (res.iters != rit[sl]))),
             "longest_pair_iters": int(res.iters.max())}
+    full = runs[n]
+    aerr = np.abs(full.err - rerr)
+    margin = np.minimum(m_eps, m_d)
+    ratio = margin / np.maximum(aerr, 1e-300)
+    worst = np.argsort(ratio)[:5]
+    out["stopping_margins"] = {
+        "definition": "per pair: min over the oracle's iterations of |err_k - eps| and ||err_{k-1} - err_k| - 1e-4|; "
+                      "abs_err_diff = |GPU err - oracle err| of the final iteration (10k run)",
+        "min_margin_eps": float(m_eps.min()), "min_margin_delta": float(m_d.min()),
+        "min_margin": float(margin.min()), "max_abs_err_diff": float(aerr.max()),
+        "min_margin_over_err_diff": float(ratio.min()),
+        "pairs_margin_below_1e3x_diff": int(np.sum(margin < 1e3 * aerr)),
+        "closest_pairs": [{"pair": int(b), "margin": float(margin[b]), "abs_err_diff": float(aerr[b]),
+                           "iters": int(rit[b])} for b in worst]}
     print(json.dumps(out, indent=1))
 
 

@@ -17,10 +17,15 @@ Closure), one beam at a time in the reference's loop order:
   positive cell sets it to -128, a hit on a negative cell to 127) — the
   restatement uses the same expressions, hence the same wrap-around.
 
-Parity: UNPINNED against the reference itself — src/produce_occupancy_grid.py
-imports cv2 at module level and OpenCV is absent here, so the module cannot be
-imported to generate fixtures; this file is checked against
-hand-derived cases in tests/test_occupancy.py instead.
+Parity: PINNED to the reference itself.  src/produce_occupancy_grid.py
+imports cv2 at module level (only ``save_image`` uses it) and OpenCV is absent
+here, so the module is not imported; tests/golden/gen_grid.py instead executes
+the reference's own grid function definitions (extracted from its source with
+``ast``: produce / update / construct_global_points / bresenham_update /
+global_position_to_grid_cell, :12-138) and stores inputs and outputs in
+tests/golden/grid_ref.npz.  tests/test_occupancy.py checks this file against
+those fixtures bit for bit (grids, origins, global points), besides
+hand-derived rays.
 """
 import numpy as np
 

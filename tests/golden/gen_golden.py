@@ -29,13 +29,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.dont_write_bytecode = True
-sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+# the reference's `src` (a namespace package: no __init__.py) must be imported
+# before the build's package directory, whose regular `src` package would win
+# the import whatever the path order, is on the path
 sys.path.insert(0, REF)
 
 import src.icp as ref_icp  # noqa: E402  (the reference)
 import src.pose_graph as ref_pg  # noqa: E402
 import src.pose_graph_optimization as ref_pgo  # noqa: E402
 import src.utils as ref_utils  # noqa: E402
+
+sys.path.append(os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
 from slamhip import synthetic  # noqa: E402
 
 assert ref_icp.__file__.startswith(REF), ref_icp.__file__

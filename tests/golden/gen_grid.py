@@ -1,0 +1,89 @@
+"""Generate tests/golden/grid_ref.npz by running the REFERENCE's occupancy-grid
+functions (/root/reference/src/produce_occupancy_grid.py).
+
+That module imports cv2 at module level (:2), which this image lacks, and cv2
+is used only by ``save_image`` (:160-162).  So instead of importing the module,
+this script parses its source with ``ast`` and executes exactly the function
+definitions the grid path needs — ``produce_occupancy_grid`` (:12-58),
+``update_occupancy_grid`` (:60-79), ``construct_global_points`` (:81-94),
+``bresenham_update`` (:96-131), ``global_position_to_grid_cell`` (:133-138) —
+in a namespace holding the real modules they name (numpy, tqdm, and the
+reference's own ``src.utils``).  No stand-in for cv2 or anything else is
+made: ``save_image`` is simply not executed.
+
+Runs only in the build container (the reference never travels to the GPU box);
+the .npz it writes holds inputs and reference outputs only (data, no code).
+
+    python tests/golden/gen_grid.py
+"""
+import ast
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+SRC = os.path.join(REF, "src", "produce_occupancy_grid.py")
+NEEDED = ("produce_occupancy_grid", "update_occupancy_grid", "construct_global_points",
+          "bresenham_update", "global_position_to_grid_cell")
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)   # the reference's `src` first (a namespace package: it must be imported
+                          # before the build's regular `src` package is on the path)
+
+
+def reference_grid_functions():
+    import tqdm as _tqdm
+
+    import src.utils as ref_utils   # the reference's own module
+    assert ref_utils.__file__.startswith(REF), ref_utils.__file__
+    tree = ast.parse(open(SRC).read(), filename=SRC)
+    defs = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in NEEDED]
+    assert sorted(d.name for d in defs) == sorted(NEEDED), [d.name for d in defs]
+    ns = {"np": np, "tqdm": _tqdm.tqdm, "utils": ref_utils}
+    exec(compile(ast.Module(body=defs, type_ignores=[]), SRC, "exec"), ns)
+    return ns
+
+
+def pack(arrs):
+    off = np.zeros(len(arrs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(a) for a in arrs])
+    return np.concatenate(arrs, axis=0), off
+
+
+def main():
+    ref = reference_grid_functions()
+    sys.path.append(os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+    from slamhip import synthetic
+    out = {}
+    cases = [  # (seed, scans, beams, cell width, hit, miss, min_width, min_height)
+        (3, 6, 181, 0.1, 3, 1, 0, 0),
+        (5, 5, 241, 0.05, 5, 2, 0, 0),
+        (8, 3, 121, 0.1, 3, 1, 30, 25),
+    ]
+    for c, (seed, n, beams, cw, kh, km, mw, mh) in enumerate(cases):
+        seq = synthetic.make_sequence(n, seed=seed, n_beams=beams)
+        poses, scans = seq.truth.copy(), [s.copy() for s in seq.scans]
+        g, (mx, my) = ref["produce_occupancy_grid"](poses, scans, cw, min_width=mw, min_height=mh,
+                                                    kHitOdds=kh, kMissOdds=km)
+        pts, off = pack(scans)
+        out[f"poses_{c}"], out[f"pts_{c}"], out[f"off_{c}"] = poses, pts, off
+        out[f"params_{c}"] = np.array([cw, kh, km, mw, mh], dtype=np.float64)
+        out[f"grid_{c}"], out[f"origin_{c}"] = g, np.array([mx, my])
+        gp, _ = pack(ref["construct_global_points"](poses, scans))
+        out[f"gpts_{c}"] = gp
+    # update_occupancy_grid on top of case 0's grid with 4 more scans of another sequence
+    seq = synthetic.make_sequence(4, seed=13, n_beams=181)
+    g0 = out["grid_0"].copy()
+    mx, my = out["origin_0"]
+    g1 = ref["update_occupancy_grid"](g0, seq.truth.copy(), [s.copy() for s in seq.scans], 0.1, mx, my)
+    pts, off = pack(seq.scans)
+    out.update(upd_poses=seq.truth.copy(), upd_pts=pts, upd_off=off, upd_grid=g1)
+    out["n_cases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, "grid_ref.npz"), **out)
+    print("wrote grid_ref.npz:", {k: v.shape for k, v in out.items() if k.startswith("grid") or k == "upd_grid"})
+
+
+if __name__ == "__main__":
+    main()

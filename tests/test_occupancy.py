@@ -1,8 +1,9 @@
 """Occupancy-grid mapper (src/produce_occupancy_grid.py): the order-free
 per-cell rule the kernel relies on (CPU, exhaustive against the sequential
-int8 rule), the oracle on hand-derived rays (CPU), and the HIP path against the
-oracle (GPU).  Parity vs the reference itself is unpinned: the reference module
-imports cv2 (absent), see oracle/occupancy_oracle.py."""
+int8 rule), the oracle on hand-derived rays (CPU), the oracle AND the HIP path
+against fixtures produced by the reference's own grid functions
+(tests/golden/grid_ref.npz, tests/golden/gen_grid.py), and the HIP path
+against the oracle on more shapes (GPU)."""
 import numpy as np
 import pytest
 
@@ -52,6 +53,55 @@ def test_oracle_single_ray():
     oo.ray_update(grid, np.array([0.05, 0.15]), np.array([0.45, 0.15]), 0.0, 0.0, 0.1, 3, 1)
     # second beam: the endpoint's miss hits a positive cell (-> -128), its hit a negative one (-> 127)
     assert grid[1].tolist() == [-2, -2, -2, -2, 127, 0, 0, 0]
+
+
+def _grid_case(g, c):
+    off = g[f"off_{c}"]
+    pts = g[f"pts_{c}"]
+    scans = [pts[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+    cw, kh, km, mw, mh = g[f"params_{c}"]
+    return g[f"poses_{c}"], scans, float(cw), int(kh), int(km), float(mw), float(mh)
+
+
+def _upd_case(g):
+    off, pts = g["upd_off"], g["upd_pts"]
+    return g["upd_poses"], [pts[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+
+
+def test_oracle_vs_reference_fixtures(golden):
+    """The oracle restatement equals the reference's produce_occupancy_grid /
+    update_occupancy_grid / construct_global_points (run by gen_grid.py in
+    the build container) bit for bit: grids, origins and global points."""
+    g = golden("grid_ref.npz")
+    for c in range(int(g["n_cases"])):
+        poses, scans, cw, kh, km, mw, mh = _grid_case(g, c)
+        r, (rx, ry) = oo.produce(poses, scans, cw, min_width=mw, min_height=mh, k_hit=kh, k_miss=km)
+        assert np.array_equal(r, g[f"grid_{c}"]) and r.dtype == np.int8, c
+        assert (rx, ry) == tuple(g[f"origin_{c}"]), c
+        assert np.array_equal(np.concatenate(oo.global_points(poses, scans)), g[f"gpts_{c}"]), c
+    assert (g["grid_0"] != 0).mean() > 0.05 and (g["grid_0"] == 127).any() and (g["grid_0"] < 0).any()
+    poses, scans = _upd_case(g)
+    r = oo.update(g["grid_0"].copy(), poses, scans, 0.1, *g["origin_0"])
+    assert np.array_equal(r, g["upd_grid"])
+
+
+@pytest.mark.gpu
+def test_produce_vs_reference_fixtures(golden):
+    """The HIP mapper equals the reference's own grid functions bit for bit
+    (tests/golden/grid_ref.npz): grid, origin, and the update of an existing
+    grid with more scans."""
+    import src.produce_occupancy_grid as pog
+    g = golden("grid_ref.npz")
+    for c in range(int(g["n_cases"])):
+        poses, scans, cw, kh, km, mw, mh = _grid_case(g, c)
+        got, (mx, my) = pog.produce_occupancy_grid(poses, scans, cw, min_width=mw, min_height=mh,
+                                                   kHitOdds=kh, kMissOdds=km)
+        assert (mx, my) == tuple(g[f"origin_{c}"]), c
+        assert got.dtype == np.int8 and np.array_equal(got, g[f"grid_{c}"]), c
+    poses, scans = _upd_case(g)
+    grid = g["grid_0"].copy()
+    pog.update_occupancy_grid(grid, poses, scans, 0.1, *g["origin_0"])
+    assert np.array_equal(grid, g["upd_grid"])
 
 
 def _scans(n, beams, seed):

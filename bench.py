@@ -212,6 +212,8 @@ def cpu_baseline(scans, inits, sample, workers):
     its = [r[2] for r in res_all]
     base = {"value": modes["ref_loop_all_cores"]["pairs_per_s"], "unit": "scan-pairs/s", "cores": workers,
             "kind": "port",
+            "cores_note": f"the job's {workers}-CPU share (n_jobs=-1 within it; OMP_NUM_THREADS caps the share on "
+                          "the GPU box), not every CPU of the host",
             "sample": f"{len(idx_all)} evenly spaced pairs of this workload (1081-pt scans, mean {np.mean(its):.1f} "
                       f"ICP iterations): oracle/icp_oracle.py with the reference's per-query loop "
                       f"(src/icp.py:16-17), joblib loky x{workers} (scripts/main.py:240 pattern)",
@@ -270,12 +272,48 @@ def pgo_bench():
         pgo_drop_in.pose_graph_optimization_step_sgd(pg, learning_rate=1.0 / (i + 2))
     dt_drop = (time.perf_counter() - t0) / k
     out = {"sgd_step_ms": round(dt * 1e3, 3), "sgd_dropin_step_ms": round(dt_drop * 1e3, 3),
-           "sgd_graph": f"{len(poses)} nodes / {len(ea)} edges", "sgd_ref_cpu_s_per_step": 138.9}
+           "sgd_graph": f"{len(poses)} nodes / {len(ea)} edges"}
     try:
         from slamhip import gn
         out.update(gn.bench_c4())
     except (ImportError, AttributeError):
         pass
+    out["cpu_baseline"] = pgo_cpu_baseline(poses, ea, eb, tf)
+    return out
+
+
+def pgo_cpu_baseline(poses, ea, eb, tf):
+    """The pose-graph CPU paths timed on this host: the SGD step
+    as the vectorised NumPy port of the reference (oracle/pgo_oracle.py,
+    src/pose_graph_optimization.py:7-49 restated; one step, 1 core) on the
+    same C4-size graph as sgd_step_ms, and the build's float64 SciPy GN
+    (oracle/gn_oracle.py) on C4, 1 BLAS thread and every thread of the job's
+    share.  The reference's own SGD code is not run here (it stays in the
+    build container); its 138.9 s/step is the survey's measurement."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import gn_oracle
+    import pgo_oracle
+    from threadpoolctl import threadpool_limits
+    from slamhip import synthetic
+    out = {}
+    with threadpool_limits(1):
+        t0 = time.perf_counter()
+        pgo_oracle.sgd_step(np.array(poses, dtype=np.float64), ea, eb, tf, 1.0)
+        out["sgd_port_1core_s_per_step"] = round(time.perf_counter() - t0, 3)
+    guess, gea, geb, gtf, _ = synthetic.lap_graph_c4()
+    its = 3
+    for name, lim in (("gn_oracle_1thread_iters_per_sec", 1), ("gn_oracle_all_threads_iters_per_sec", None)):
+        with threadpool_limits(lim):
+            t0 = time.perf_counter()
+            gn_oracle.optimize(guess.copy(), gea, geb, gtf, iterations=its)
+            out[name] = round(its / (time.perf_counter() - t0), 3)
+    out.update({"threads_all": default_cpu_workers(), "kind": "port",
+                "sgd_reference_s_per_step_survey": 138.9,
+                "note": "sgd_port: oracle/pgo_oracle.py (vectorised, bit-exact with the reference) on the "
+                        f"{len(poses)}-node / {len(ea)}-edge graph; gn_oracle: SciPy SuperLU GN on C4 "
+                        "(5000 nodes / 20000 edges); sgd_reference_s_per_step_survey: the reference's own "
+                        "src/pose_graph_optimization.py, 1 core of the build container (SURVEY.md §6), not "
+                        "re-run on this box"})
     return out
 
 

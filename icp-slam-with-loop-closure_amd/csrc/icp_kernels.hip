@@ -42,7 +42,8 @@ __device__ int g_icp_status;                // nonzero: some pair was outside it
 // two reduction slabs of 16 doubles per wave at the front of the dynamic LDS
 // (block_sum_exact16, alternating between iterations), then 16 doubles of
 // per-pair constants (kept in LDS, not in registers across the NN search)
-constexpr int kPairConsts = 32;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab
+constexpr int kPairConsts = 34;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab (16 sums + the
+                                  // arrival flag; an even count keeps the candidates 16-byte aligned)
 __host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 16 + kPairConsts; }
 enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kBcast = 16 };
 
@@ -83,6 +84,7 @@ struct IcpArgs {
     int32_t gang;
     int32_t n_gangs;
     uint64_t* gang_slots;    // [n_gangs][2][gang][32] tagged granules, zeroed before the launch
+    uint32_t gang_wait;      // longest wait for the partners of one exchange (s_memrealtime ticks)
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
 #ifndef SLAM_TAIL_SHARE
@@ -90,8 +92,12 @@ constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 gr
 #endif
 constexpr size_t kTailShare = SLAM_TAIL_SHARE;   // gang / team workgroups per CU (LDS requested: kMaxLds / share)
 constexpr int kGangSweep = 32;        // parts an exchange sweep covers (16 loads per lane)
-constexpr uint32_t kGangSpinLimit = 1u << 26;   // ~seconds of polling: a lost partner ends the launch
-__device__ int g_gang_timeout;        // set when a gang partner never arrived
+// A gang exchange waits at most this many s_memrealtime ticks (100 MHz) for its
+// partners; a part that times out stops at once (the timeout is sticky: it
+// never waits again), writes nothing, and the pair is re-run from its saved
+// phase-1 state on one workgroup after the phase (launch_batch's repair launch)
+constexpr uint32_t kGangWaitTicks = 20000000;   // 0.2 s
+__device__ int g_gang_timeout;        // parts that timed out (read-and-cleared by slam_icp_gang_timeouts)
 
 // A wave-uniform double moved to SGPRs (v_readfirstlane of both halves).
 __device__ __forceinline__ double uniform_d(double v) {
@@ -542,12 +548,15 @@ __device__ __forceinline__ bool certify(double d1, double s2, double a) {
 // (N per lane, addresses clamped so every load is issued unconditionally),
 // repeated until every tag matches; then the doubles reassembled across the
 // lane halves (lane l ^ 16 holds the other half) and summed.  Own granules come
-// from registers.
+// from registers.  `arrived` (wave-uniform) turns false when the partners did
+// not all arrive within `wait` s_memrealtime ticks; the sum is then garbage.
 template <int N>
 __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp, int part, int parts, uint64_t tag,
-                                             uint32_t own, int lane) {
+                                             uint32_t own, int lane, uint32_t wait, bool& arrived) {
     uint32_t v[N];
-    for (uint32_t spins = 0;;) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    arrived = true;
+    for (;;) {
         uint64_t x[N];
 #pragma unroll
         for (int k = 0; k < N; ++k)
@@ -562,8 +571,9 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
         }
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > kGangSpinLimit) {   // a partner never arrived: flag it, end in finite time
-            if (lane == 0) atomicOr(&g_gang_timeout, 1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > wait) {   // a partner never arrived
+            if (lane == 0) atomicAdd(&g_gang_timeout, 1);
+            arrived = false;
             break;
         }
     }
@@ -590,36 +600,52 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
 // part's e + 1 granules, each published after its reader finished exchange e.
 // (One exchange ~2 L2-miss round trips; the counter form it replaced took
 // four: store, drain, counter add, poll.)
-__device__ __forceinline__ double gang_exchange(double t, uint64_t* slots, int part, int parts, int e, double* bcast) {
+// One wave's part of the exchange: publish this part's granules, sweep every
+// part's until they all arrived (or `wait` ran out: arrived = false), and
+// return the total of value q in lane q < 16.  Called by ONE wave per part.
+__device__ __forceinline__ double gang_exchange_wave(double t, uint64_t* slots, int part, int parts, int e,
+                                                     uint32_t wait, bool& arrived) {
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const uint64_t tag = static_cast<uint64_t>(e + 1) << 32;
     uint64_t* buf = slots + (e & 1) * parts * 32;
     const uint64_t tb = static_cast<uint64_t>(__double_as_longlong(__shfl(t, lane & 15, 64)));
-    if (wave == 0 && lane < 32)
+    if (lane < 32)
         __hip_atomic_store(buf + part * 32 + lane, tag | ((lane & 16) ? (tb >> 32) : (tb & 0xffffffffull)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wave == 0) {   // one polling wave per workgroup (every wave polling queued the last arriver's loads)
-        const int g = lane & 31, pp = lane >> 5;
-        const uint32_t own = static_cast<uint32_t>((lane & 16) ? (tb >> 32) : tb);
-        double s = 0.0;
-        // branch-free sweeps of N loads per lane (a divergent guard around each
-        // load made the compiler drain them one by one)
-        if (parts <= 4)
-            s = gang_sweep<2>(buf, g, pp, part, parts, tag, own, lane);
-        else if (parts <= 8)
-            s = gang_sweep<4>(buf, g, pp, part, parts, tag, own, lane);
-        else if (parts <= 16)
-            s = gang_sweep<8>(buf, g, pp, part, parts, tag, own, lane);
-        else
-            s = gang_sweep<kGangSweep / 2>(buf, g, pp, part, parts, tag, own, lane);
-        s += __shfl_xor(s, 32, 64);   // parts of even + odd index (the same bits in both halves)
+    const int g = lane & 31, pp = lane >> 5;
+    const uint32_t own = static_cast<uint32_t>((lane & 16) ? (tb >> 32) : tb);
+    double s = 0.0;
+    // branch-free sweeps of N loads per lane (a divergent guard around each
+    // load made the compiler drain them one by one)
+    if (parts <= 4)
+        s = gang_sweep<2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+    else if (parts <= 8)
+        s = gang_sweep<4>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+    else if (parts <= 16)
+        s = gang_sweep<8>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+    else
+        s = gang_sweep<kGangSweep / 2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+    return s + __shfl_xor(s, 32, 64);   // parts of even + odd index (the same bits in both halves)
+}
+
+// Block-wide exchange: wave 0 polls (every wave polling queued the last
+// arriver's loads) and broadcasts the sums and the arrival flag through LDS.
+// Returns false in every thread when a partner timed out.
+__device__ __forceinline__ bool gang_exchange(double& t, uint64_t* slots, int part, int parts, int e, uint32_t wait,
+                                             double* bcast) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    if (wave == 0) {
+        bool arrived;
+        const double s = gang_exchange_wave(t, slots, part, parts, e, wait, arrived);
         if (lane < 16) bcast[lane] = s;
+        if (lane == 0) bcast[16] = arrived ? 1.0 : 0.0;
     }
     // the slab is rewritten only at the next exchange, after the next
     // block_sum_exact16 barrier, so every wave has read it by then
     __syncthreads();
-    return lane < 16 ? bcast[lane] : 0.0;
+    t = lane < 16 ? bcast[lane] : 0.0;
+    return bcast[16] != 0.0;
 }
 
 // Per-pair setup shared by the kernels: pc2 into LDS (fp64, fp32 pairs with
@@ -1154,9 +1180,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
         }
         if constexpr (GANG) {
-            if (parts > 1)
-                tot = gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part, parts,
-                                    it - it0, pconst + kBcast);
+            // a partner that never arrived: stop at once, write nothing (the
+            // repair launch re-runs the pair from its phase-1 state)
+            if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
+                                            parts, it - it0, a.gang_wait, pconst + kBcast))
+                return;
         }
         const double n = static_cast<double>(n1);
         const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
@@ -1602,9 +1630,11 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
             }
             tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
             tstamp(7);
-            if (parts > 1)
-                tot = gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part, parts,
-                                    it - it0, pconst + kBcast);
+            if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
+                                            parts, it - it0, a.gang_wait, pconst + kBcast)) {
+                tflush();
+                return;   // a partner timed out: nothing written, the repair launch re-runs the pair
+            }
         }
         tstamp(8);
         const double n = static_cast<double>(n1);
@@ -1900,6 +1930,7 @@ static const Instance* pick_head_instance(int max_n1) {
 // workgroup's.  Results are bit-identical.
 static int g_sched_gangs = 24;
 static int g_sched_gang_parts = 4;
+static uint32_t g_gang_wait = kGangWaitTicks;   // diagnostics can shorten it to force timeouts
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
@@ -1938,6 +1969,7 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
         a.gang = parts;
         a.n_gangs = G;
         a.gang_slots = slots;
+        a.gang_wait = g_gang_wait;
         const size_t lds_need = red_doubles(kTeamBlock) * sizeof(double) +
                                 static_cast<size_t>(a.cand_cap) * (sizeof(double2) + sizeof(float2)) +
                                 static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) + team_xbuf_words() * sizeof(uint32_t);
@@ -1957,6 +1989,7 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
     a.gang = parts;
     a.n_gangs = G;
     a.gang_slots = slots;
+    a.gang_wait = g_gang_wait;
     const size_t lds_need = red_doubles(gi->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2) +
                             static_cast<size_t>(a.cand_cap) * sizeof(float2) +
                             static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
@@ -1970,37 +2003,104 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
     return check_launch("icp gang kernel");
 }
 
-__global__ __launch_bounds__(256) void sched_count_kernel(const int32_t* __restrict__ iters,
-                                                          const float* __restrict__ key, int32_t B,
-                                                          float thresh, int32_t* __restrict__ hist,
-                                                          int32_t* __restrict__ bucket) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= B) return;
-    int q = kSchedBuckets;   // finished pairs go last (their workgroups exit at once)
-    if (iters[b] <= 0) {
-        const float l = log2f(fmaxf(key[b] / thresh, 1e-30f));   // 8 buckets per octave, 2^16 -> 0
-        q = min(max(static_cast<int>(floorf(128.0f - 8.0f * l)), 0), kSchedBuckets - 1);
-    }
-    bucket[b] = q;
-    atomicAdd(&hist[q], 1);
+// Stable counting sort of the pairs by bucket, so order[] (which pairs become
+// gangs, heads, bulk) is the same every run: per block of kSortBlock pairs a
+// histogram hist_blk[blk][q] (LDS atomics: counts are order-free), an
+// exclusive scan over (bucket, block) in bucket-major order, then a scatter
+// where a pair lands at its (bucket, block) offset plus the number of earlier
+// pairs of its block in the same bucket (wave match loop + per-wave counts).
+constexpr int kSortBlock = 1024;
+constexpr int kNB = kSchedBuckets + 1;   // buckets incl. "finished"
+constexpr int kScanChunk = 32;           // blocks per LDS chunk of the scan (32 KB)
+
+__device__ __forceinline__ int sched_bucket(const int32_t* iters, const float* key, int b, float thresh) {
+    if (iters[b] > 0) return kSchedBuckets;   // finished pairs go last (their workgroups exit at once)
+    const float l = log2f(fmaxf(key[b] / thresh, 1e-30f));   // 8 buckets per octave, 2^16 -> 0
+    return min(max(static_cast<int>(floorf(128.0f - 8.0f * l)), 0), kSchedBuckets - 1);
 }
 
-__global__ __launch_bounds__(64) void sched_scan_kernel(int32_t* __restrict__ hist) {
-    if (threadIdx.x != 0) return;   // 257 counters: one lane is plenty
-    int s = 0;
-    for (int q = 0; q <= kSchedBuckets; ++q) {
-        const int c = hist[q];
-        hist[q] = s;
-        s += c;
+__global__ __launch_bounds__(kSortBlock) void sched_count_kernel(const int32_t* __restrict__ iters,
+                                                                 const float* __restrict__ key, int32_t B,
+                                                                 float thresh, int32_t* __restrict__ hist_blk,
+                                                                 int32_t* __restrict__ bucket) {
+    __shared__ int h[kNB];
+    for (int q = threadIdx.x; q < kNB; q += kSortBlock) h[q] = 0;
+    __syncthreads();
+    const int b = blockIdx.x * kSortBlock + threadIdx.x;
+    if (b < B) {
+        const int q = sched_bucket(iters, key, b, thresh);
+        bucket[b] = q;
+        atomicAdd(&h[q], 1);
     }
+    __syncthreads();
+    for (int q = threadIdx.x; q < kNB; q += kSortBlock) hist_blk[blockIdx.x * kNB + q] = h[q];
 }
 
-__global__ __launch_bounds__(256) void sched_scatter_kernel(const int32_t* __restrict__ bucket, int32_t B,
-                                                            int32_t* __restrict__ offs,
-                                                            int32_t* __restrict__ order) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= B) return;
-    order[atomicAdd(&offs[bucket[b]], 1)] = b;
+// One workgroup: hist_blk[blk][q] <- sum of the counts of all (q' < q, any
+// block) and (q, blk' < blk): the first slot of (bucket q, block blk).
+__global__ __launch_bounds__(512) void sched_scan_kernel(int32_t* __restrict__ hist_blk, int32_t nblk) {
+    __shared__ int chunk[kScanChunk * kNB];
+    __shared__ int tot[512];
+    const int q = threadIdx.x;
+    int run = 0;   // column q's running count over the blocks
+    for (int k0 = 0; k0 < nblk; k0 += kScanChunk) {
+        const int nk = min(kScanChunk, nblk - k0);
+        for (int i = threadIdx.x; i < nk * kNB; i += 512) chunk[i] = hist_blk[k0 * kNB + i];   // coalesced, in flight
+        __syncthreads();
+        if (q < kNB) {
+            for (int k = 0; k < nk; ++k) {
+                const int c = chunk[k * kNB + q];
+                chunk[k * kNB + q] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nk * kNB; i += 512) hist_blk[k0 * kNB + i] = chunk[i];
+        __syncthreads();
+    }
+    // exclusive scan of the bucket totals (Hillis-Steele over 512 slots)
+    tot[q] = q < kNB ? run : 0;
+    __syncthreads();
+    for (int d = 1; d < 512; d <<= 1) {
+        const int v = q >= d ? tot[q - d] : 0;
+        __syncthreads();
+        tot[q] += v;
+        __syncthreads();
+    }
+    const int base = q < kNB ? tot[q] - run : 0;
+    __syncthreads();
+    tot[q] = base;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nblk * kNB; i += 512) hist_blk[i] += tot[i % kNB];
+}
+
+__global__ __launch_bounds__(kSortBlock) void sched_scatter_kernel(const int32_t* __restrict__ bucket, int32_t B,
+                                                                   const int32_t* __restrict__ hist_blk,
+                                                                   int32_t* __restrict__ order) {
+    constexpr int WAVES = kSortBlock / 64;
+    __shared__ int cnt[WAVES * kNB];
+    for (int i = threadIdx.x; i < WAVES * kNB; i += kSortBlock) cnt[i] = 0;
+    __syncthreads();
+    const int b = blockIdx.x * kSortBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool valid = b < B;
+    const int q = valid ? bucket[b] : -1;
+    // rank among the wave's lanes with the same bucket: one ballot per distinct bucket
+    int rank = 0;
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+        const int u = __shfl(q, static_cast<int>(__builtin_ctzll(todo)), 64);
+        const uint64_t m = __ballot(q == u);
+        if (q == u) rank = __popcll(m & ((1ull << lane) - 1));
+        if (lane == 0) cnt[wave * kNB + u] = __popcll(m);
+        todo &= ~m;
+    }
+    __syncthreads();
+    if (valid) {
+        int pos = hist_blk[blockIdx.x * kNB + q] + rank;
+        for (int w = 0; w < wave; ++w) pos += cnt[w * kNB + q];
+        order[pos] = b;
+    }
 }
 
 static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2, void* stream) {
@@ -2020,12 +2120,14 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                          (team ? parts <= kTeamMaxParts : parts >= 2 && pick_gang_instance(max_n1, parts) != nullptr);
     const int G = gang_ok ? min(g_sched_gangs, heads) : 0;
     const size_t gang_slot_bytes = static_cast<size_t>(G) * 2 * max(parts, 1) * 32 * sizeof(uint64_t);
-    const size_t sched_bytes = ((kSchedBuckets + 1) * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float)) + 255) / 256 * 256;
+    const int nblk = (B + kSortBlock - 1) / kSortBlock;
+    const size_t sched_bytes =
+        (static_cast<size_t>(nblk) * kNB * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float)) + 255) / 256 * 256;
     const size_t bytes = sched_bytes + gang_slot_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
-    int32_t* hist = static_cast<int32_t*>(ws);
-    int32_t* bucket = hist + kSchedBuckets + 1;
+    int32_t* hist = static_cast<int32_t*>(ws);   // hist_blk[nblk][kNB]
+    int32_t* bucket = hist + static_cast<size_t>(nblk) * kNB;
     int32_t* order = bucket + nb;
     float* key = reinterpret_cast<float*>(order + nb);
     uint64_t* gang_slots = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes);
@@ -2034,13 +2136,12 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     a.sched_key = key;
     int rc = launch(false, a, B, max_n1, max_n2, stream);
     if (rc == 0) {
-        const int g = (B + 255) / 256;
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
-        (void)hipMemsetAsync(hist, 0, (kSchedBuckets + 1) * sizeof(int32_t), s);
         if (G > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
-        hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(256), 0, s, args.out_iters, key, B, thr, hist, bucket);
-        hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(64), 0, s, hist);
-        hipLaunchKernelGGL(sched_scatter_kernel, dim3(g), dim3(256), 0, s, bucket, B, hist, order);
+        hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr, hist,
+                           bucket);
+        hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
+        hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, s, bucket, B, hist, order);
         rc = check_launch("icp scheduler kernels");
     }
     if (rc == 0) {   // phase 2: the unfinished pairs, slowest-converging first
@@ -2076,6 +2177,15 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             if (rc == 0 && (hipStreamWaitEvent(s, side->join, 0) != hipSuccess ||
                             hipStreamWaitEvent(s, side->join2, 0) != hipSuccess))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
+            if (rc == 0 && G > 0) {
+                // repair: a gang whose partners did not all arrive stopped without
+                // writing, leaving its pair paused at the phase-1 state; re-run
+                // such pairs on one workgroup each (finished pairs' workgroups
+                // exit at once, so this costs one near-empty launch)
+                IcpArgs r = a;
+                r.order = order;
+                rc = launch(false, r, G, max_n1, max_n2, stream);
+            }
         } else {
             rc = launch(false, a, B, max_n1, max_n2, stream);
         }
@@ -2132,10 +2242,45 @@ int slam_icp_set_schedule_gangs(int gangs, int parts) {
     g_sched_gang_parts = parts;
     return ok();
 }
+// Gang parts that timed out waiting for a partner since the last call (their
+// pairs were re-run on single workgroups: results stay valid); read-and-clear.
+// Synchronises the device.
 int slam_icp_gang_timeouts(void) {
     int v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_gang_timeout), sizeof(int)) != hipSuccess) return fail(SLAM_EHIP, "gang timeouts: read");
+    const int zero = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_gang_timeout), sizeof(int)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_gang_timeout), &zero, sizeof(int)) != hipSuccess)
+        return fail(SLAM_EHIP, "gang timeouts: read");
     return v;
+}
+// Diagnostics: the longest wait of a gang exchange for its partners, in
+// s_memrealtime ticks (100 MHz); 0 restores the default (0.2 s).  Tiny values
+// force timeouts (the repair path).
+int slam_icp_set_gang_wait(uint32_t ticks) {
+    g_gang_wait = ticks ? ticks : kGangWaitTicks;
+    return ok();
+}
+// Diagnostics: the scheduler's stable bucket sort on its own: order[] of B
+// pairs from their phase-1 out_iters and keys (device arrays), as phase 2
+// would visit them.
+int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float thresh, int32_t* order,
+                        void* stream) {
+    if (B <= 0) return ok();
+    if (!iters || !key || !order) return fail(SLAM_EINVAL, "null array argument");
+    hipStream_t s = as_stream(stream);
+    const int nblk = (B + kSortBlock - 1) / kSortBlock;
+    void* ws = nullptr;
+    const size_t bytes = (static_cast<size_t>(nblk) * kNB + static_cast<size_t>(B)) * sizeof(int32_t);
+    if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "sched sort: no workspace");
+    int32_t* hist = static_cast<int32_t*>(ws);
+    int32_t* bucket = hist + static_cast<size_t>(nblk) * kNB;
+    hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, iters, key, B, thresh, hist, bucket);
+    hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
+    hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, s, bucket, B, hist, order);
+    const int rc = check_launch("sched sort kernels");
+    (void)hipFreeAsync(ws, s);
+    return rc;
 }
 int slam_icp_set_schedule(int probe_iters, int min_pairs) {
     if (probe_iters < 0 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: negative argument");
@@ -2149,15 +2294,9 @@ int slam_icp_set_schedule(int probe_iters, int min_pairs) {
 // out_err NaN), then clears the flag.
 int slam_icp_status(void* stream) {
     if (hipStreamSynchronize(as_stream(stream)) != hipSuccess) return fail(SLAM_EHIP, "icp status: stream sync");
-    int st = 0, gt = 0;
-    if (hipMemcpyFromSymbol(&st, HIP_SYMBOL(g_icp_status), sizeof(int)) != hipSuccess ||
-        hipMemcpyFromSymbol(&gt, HIP_SYMBOL(g_gang_timeout), sizeof(int)) != hipSuccess)
+    int st = 0;
+    if (hipMemcpyFromSymbol(&st, HIP_SYMBOL(g_icp_status), sizeof(int)) != hipSuccess)
         return fail(SLAM_EHIP, "icp status: read");
-    if (gt != 0) {
-        const int zero = 0;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gang_timeout), &zero, sizeof(int));
-        return fail(SLAM_EHIP, "icp: a gang's workgroups were not co-resident (partner timeout); results invalid");
-    }
     if (st == 0) return ok();
     const int zero = 0;
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_icp_status), &zero, sizeof(int));

@@ -222,10 +222,21 @@ int slam_icp_set_schedule_heads(int heads);
  * bit-identical to the one-workgroup kernels.  gangs = 0: off; defaults
  * (24, 4).  SLAM_EINVAL for gangs < 0, parts 1, < 0 or > 17. */
 int slam_icp_set_schedule_gangs(int gangs, int parts);
-/* Nonzero if a gang's workgroups ever failed to meet (a partner not resident
- * for ~seconds; the launch then ended without valid results).  slam_icp_status
- * reports and clears it as SLAM_EHIP. */
+/* Gang parts that waited longer than the gang wait (default 0.2 s) for a
+ * partner since the last call (read-and-clear; synchronises the device).  Such
+ * a part stops at once without writing; after phase 2 the scheduler re-runs
+ * every gang pair that did not finish on one workgroup from its saved phase-1
+ * state, so the results stay valid (and bit-identical): this count is a
+ * warning, not an error.  Scheduler order is a stable sort (deterministic). */
 int slam_icp_gang_timeouts(void);
+/* Diagnostics: the gang wait in s_memrealtime ticks (100 MHz); 0 = default.
+ * Tiny values force timeouts, exercising the repair path. */
+int slam_icp_set_gang_wait(uint32_t ticks);
+/* Diagnostics: phase 2's visiting order of B pairs from their phase-1
+ * out_iters (> 0: finished) and keys (last |dE|), by the scheduler's stable
+ * bucket sort (device arrays; order[] receives B pair indices). */
+int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float thresh, int32_t* order,
+                        void* stream);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver: 0 auto (block cyclic reduction when the band allows it),
  * 1 band Cholesky, 2 block cyclic reduction (falls back to 1 if not allowed). */

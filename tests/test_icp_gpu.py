@@ -454,6 +454,68 @@ def test_gangs_are_bit_identical(k):
     assert np.array_equal(ro.tf, ro_single.tf) and np.array_equal(ro.err, ro_single.err)
 
 
+def test_gang_timeouts_are_repaired(k):
+    """A gang part that waits too long for its partners stops without writing;
+    after phase 2 the scheduler re-runs every unfinished gang pair on one
+    workgroup from its phase-1 state.  With the wait forced down to one tick
+    (timeouts in most exchanges) the results are still bit-identical to the
+    single launch, for gangs and for teams, and the timeouts are reported."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 1100
+    seq, inits = _sequence_pairs(n, seed=2025)
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    try:
+        assert lib.slam_icp_set_schedule(0, 1024) == 0
+        single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+        assert lib.slam_icp_set_schedule(4, 1024) == 0
+        assert lib.slam_icp_set_gang_wait(1) == 0
+        lib.slam_icp_gang_timeouts()   # clear
+        for gangs, parts in ((64, 4), (16, 0)):
+            assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
+            r = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+            assert lib.slam_icp_gang_timeouts() > 0, (gangs, parts)
+            assert np.array_equal(r.iters, single.iters), (gangs, parts)
+            assert np.array_equal(r.tf, single.tf) and np.array_equal(r.err, single.err), (gangs, parts)
+            for h0, h1 in zip(single.hist, r.hist):
+                assert np.array_equal(h0, h1), (gangs, parts)
+    finally:
+        lib.slam_icp_set_gang_wait(0)
+        lib.slam_icp_set_schedule(4, 1024)
+        lib.slam_icp_set_schedule_gangs(24, 4)
+    assert lib.slam_icp_gang_timeouts() == 0
+
+
+def test_scheduler_order_is_a_stable_sort():
+    """Phase 2's visiting order is the scheduler's stable bucket sort: the same
+    permutation every run, unfinished pairs by bucket of log2 |dE| (largest
+    |dE| first, 8 buckets per octave), pair index ascending inside a bucket,
+    finished pairs last in index order."""
+    import ctypes
+    import torch
+    from slamhip import _abi
+    lib = _abi.lib()
+    rng = np.random.default_rng(4)
+    B, thresh = 5000, 1e-4
+    kq = rng.integers(-40, 120, B)                             # bucket 128 - 8 log2(key / thresh) = 127 - kq
+    key = (thresh * np.exp2((kq + 0.5) / 8.0)).astype(np.float32)   # mid-bucket: no rounding ambiguity
+    iters = np.where(rng.random(B) < 0.2, 7, -4).astype(np.int32)  # 20 % finished in phase 1
+    dev = torch.device("cuda", 0)
+    d_it = torch.tensor(iters, device=dev)
+    d_key = torch.tensor(key, device=dev)
+    outs = []
+    for _ in range(3):
+        d_ord = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        assert lib.slam_icp_sched_sort(ctypes.c_void_p(d_it.data_ptr()), ctypes.c_void_p(d_key.data_ptr()), B,
+                                       ctypes.c_float(thresh), ctypes.c_void_p(d_ord.data_ptr()), None) == 0
+        torch.cuda.synchronize()
+        outs.append(d_ord.cpu().numpy())
+    assert all(np.array_equal(o, outs[0]) for o in outs[1:])
+    bucket = np.where(iters > 0, 256, np.clip(127 - kq, 0, 255))
+    want = np.lexsort((np.arange(B), bucket))
+    assert np.array_equal(outs[0], want)
+
+
 def test_default_schedule_c3_shape_vs_oracle(k, oracle):
     """The benchmarked path itself: 2,400 consecutive pairs of 1081-point scans
     (the C3 stream generator, seed 2025) through the DEFAULT two-phase

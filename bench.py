@@ -78,6 +78,10 @@ def parse():
                    help="pairs started on CU-exclusive workgroups in phase 2 (-1 = library default)")
     p.add_argument("--sched-gangs", default="",
                    help="G,K: the first G head pairs run as gangs of K workgroups (library default 24,4; 0,2 = off)")
+    p.add_argument("--sched-wide", default="",
+                   help="W,S: the W slowest-keyed pairs on the wide tier, 1/S of a CU's LDS each (0,1 = off)")
+    p.add_argument("--bulk-gangs", default="",
+                   help="B,K: batches below B pairs run their bulk as gangs of K workgroups (0,2 = off)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
     return p.parse_args()
 
@@ -366,6 +370,12 @@ def main():
     if args.sched_gangs:
         g_, k_ = (int(x) for x in args.sched_gangs.split(","))
         lib.slam_icp_set_schedule_gangs(g_, k_)
+    if args.sched_wide:
+        w_, s_ = (int(x) for x in args.sched_wide.split(","))
+        lib.slam_icp_set_schedule_wide(w_, s_)
+    if args.bulk_gangs:
+        b_, k_ = (int(x) for x in args.bulk_gangs.split(","))
+        lib.slam_icp_set_bulk_gangs(b_, k_)
     lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)

@@ -258,4 +258,29 @@ __device__ __forceinline__ double block_sum_exact16(double (&v)[16], double* sla
     return t;
 }
 
+// The wave-level form of block_sum_exact16: the 16 values summed over this
+// wave's 64 lanes (exact partial sums, so the order is free), value q returned
+// in lane q < 16 — no LDS, no barrier.
+__device__ __forceinline__ double wave_sum_exact16(double (&v)[16]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        swap32_d(v[2 * j], v[2 * j + 1]);
+        v[j] = v[2 * j] + v[2 * j + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        swap16_d(v[2 * i], v[2 * i + 1]);
+        v[i] = v[2 * i] + v[2 * i + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = row_sum_d(v[i]);   // row r, register i: value 4 i + q0(r)
+    const int lane = threadIdx.x & 63;
+    const int q = lane & 15, q0 = q & 3;
+    const int src = 16 * (((q0 & 1) << 1) | (q0 >> 1));   // the row holding value q (q0 is an involution)
+    const double t0 = __shfl(v[0], src, 64), t1 = __shfl(v[1], src, 64);
+    const double t2 = __shfl(v[2], src, 64), t3 = __shfl(v[3], src, 64);
+    const int i = q >> 2;
+    return i == 0 ? t0 : i == 1 ? t1 : i == 2 ? t2 : t3;
+}
+
 }  // namespace slamhip

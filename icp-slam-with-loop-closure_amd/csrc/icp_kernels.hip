@@ -70,6 +70,10 @@ struct IcpArgs {
     unsigned long long* stamps;
     // diagnostics: total candidate evaluations performed, all lanes (NULL = off)
     unsigned long long* evals;
+    // diagnostics: per pair and phase (resume 0 / 1) the s_memrealtime (100 MHz)
+    // at which its (part-0) workgroup started and ended, and the XCC / SE / CU
+    // it ran on: trace[(b * 2 + resume) * 4 + {0: start, 1: end, 2: hw id}] (NULL = off)
+    unsigned long long* trace;
     // phased scheduling (batch mode): workgroup -> pair map (NULL = identity),
     // iterations per pair in this launch (0 = to completion), resume from the
     // state a previous phase saved in out_tf / out_err / out_iters, and the
@@ -118,6 +122,12 @@ __device__ __forceinline__ double bcast_d(double v, int src) {
 __device__ __forceinline__ float uniform_f(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
+
+// Bare v_sqrt_f32 (about 1 ulp), without the ~15-instruction IEEE rounding
+// fix-up sqrtf compiles to.  Every use below takes a bound with a relative
+// slack of >= 1e-6 (>> 1 ulp); a denormal input may flush to 0, which only
+// loosens a lower bound, and the certification's upper bound adds 1e-30 first.
+__device__ __forceinline__ float sqrt_bound(float x) { return __builtin_amdgcn_sqrtf(x); }
 
 // Squared distance with NumPy's rounding: sum((pc2[j] - q)**2) over x, y (+0).
 __device__ __forceinline__ double exact_d2(double px, double py, double qx, double qy) {
@@ -204,36 +214,61 @@ __device__ __forceinline__ void nn_scan_chunked(const float2* __restrict__ candf
     }
 }
 
+// Diagnostics trace (IcpArgs::trace): the hardware location of this wave,
+// XCC id << 16 | HW_ID (CU, SH, SE bits).
+__device__ __forceinline__ unsigned long long hw_where() {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));        // HW_REG_HW_ID, all 32 bits
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));      // HW_REG_XCC_ID, 16 bits
+    return (static_cast<unsigned long long>(xcc & 0xf) << 32) | hw;
+}
+__device__ __forceinline__ void trace_mark(const IcpArgs& a, int b, int what) {
+    if (a.trace) {
+        unsigned long long* t = a.trace + (static_cast<int64_t>(b) * 2 + (a.resume ? 1 : 0)) * 4;
+        t[what] = __builtin_amdgcn_s_memrealtime();
+        if (what == 0) t[2] = hw_where();
+    }
+}
+
 // Wave-wide min / max / or without LDS or SGPR round trips: DPP butterflies
 // inside each 16-lane row, then the gfx950 row swaps (v_permlane16_swap pairs
 // rows 0-1 and 2-3, v_permlane32_swap the two halves).  Every lane returns the
 // result.
-#define SLAM_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
-__device__ __forceinline__ float cross_rows_min(float v) {
-    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fminf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+// Min / max run on integers: a float's bits map to an int of the same order
+// (sign-magnitude -> two's complement, an involution), and non-negative floats
+// order as their unsigned bits.  An integer min takes the DPP operand directly
+// (v_min_i32_dpp, bound_ctrl: one instruction per step), where fminf would
+// canonicalise both operands first (IEEE mode) behind a separate DPP move.
+__device__ __forceinline__ int f2ord(float f) {
+    const int i = __float_as_int(f);
+    return i ^ ((i >> 31) & 0x7fffffff);
 }
-__device__ __forceinline__ float cross_rows_max(float v) {
-    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+__device__ __forceinline__ float ord2f(int o) { return __int_as_float(o ^ ((o >> 31) & 0x7fffffff)); }
+#define SLAM_DPPI(v, ctrl) __builtin_amdgcn_mov_dpp((v), (ctrl), 0xF, 0xF, true)
+template <typename I, typename Op>
+__device__ __forceinline__ I wave_reduce_i(I v, Op op) {
+    v = op(v, static_cast<I>(SLAM_DPPI(static_cast<int>(v), 0xB1)));    // quad_perm [1,0,3,2]
+    v = op(v, static_cast<I>(SLAM_DPPI(static_cast<int>(v), 0x4E)));    // quad_perm [2,3,0,1]
+    v = op(v, static_cast<I>(SLAM_DPPI(static_cast<int>(v), 0x124)));   // row_ror:4
+    v = op(v, static_cast<I>(SLAM_DPPI(static_cast<int>(v), 0x128)));   // row_ror:8
+    const auto p = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(v), static_cast<uint32_t>(v), false, false);
+    v = op(static_cast<I>(p[0]), static_cast<I>(p[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(v), static_cast<uint32_t>(v), false, false);
+    return op(static_cast<I>(q[0]), static_cast<I>(q[1]));
 }
-__device__ __forceinline__ float wave_min_f(float v) {
-    v = fminf(v, SLAM_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
-    v = fminf(v, SLAM_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
-    v = fminf(v, SLAM_DPP(v, 0x124));   // row_ror:4
-    v = fminf(v, SLAM_DPP(v, 0x128));   // row_ror:8
-    return cross_rows_min(v);
+#undef SLAM_DPPI
+struct MinI { __device__ int operator()(int a, int b) const { return min(a, b); } };
+struct MaxI { __device__ int operator()(int a, int b) const { return max(a, b); } };
+struct MinU { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return min(a, b); } };
+struct MaxU { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); } };
+// every lane returns the wave's min / max (no NaN inputs)
+__device__ __forceinline__ float wave_min_f(float v) { return ord2f(wave_reduce_i<int>(f2ord(v), MinI())); }
+__device__ __forceinline__ float wave_max_f(float v) { return ord2f(wave_reduce_i<int>(f2ord(v), MaxI())); }
+// the same for v >= 0 (or +inf)
+__device__ __forceinline__ float wave_min_nn(float v) {
+    return __uint_as_float(wave_reduce_i<uint32_t>(__float_as_uint(v), MinU()));
 }
-__device__ __forceinline__ float wave_max_f(float v) {
-    v = fmaxf(v, SLAM_DPP(v, 0xB1));
-    v = fmaxf(v, SLAM_DPP(v, 0x4E));
-    v = fmaxf(v, SLAM_DPP(v, 0x124));
-    v = fmaxf(v, SLAM_DPP(v, 0x128));
-    return cross_rows_max(v);
+__device__ __forceinline__ float wave_max_nn(float v) {
+    return __uint_as_float(wave_reduce_i<uint32_t>(__float_as_uint(v), MaxU()));
 }
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
     v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
@@ -246,7 +281,6 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
     // wave-uniform by construction: move to an SGPR for the scalar loop over its bits
     return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(q[0] | q[1])));
 }
-#undef SLAM_DPP
 
 // Conservative squared distance between two axis-aligned boxes (or a point,
 // as a degenerate box), rounded DOWN by 1e-6 relative: a lower bound of every
@@ -292,6 +326,13 @@ constexpr int kWpe = 4;          // waves/SIMD the default 1081-point instance i
 constexpr int kWinBits = 5;   // kWin * kSub = 32 window offsets
 constexpr uint32_t kWinLow = (1u << kWinBits) - 1;
 static_assert(kWin * kSub == 1 << kWinBits, "window offsets fill the key's low bits");
+// (a & m) | b as ONE v_and_or_b32 (the compiler turns the or of disjoint bits
+// into an add and fuses it with the loop offset: two instructions)
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(m), "s"(b));
+    return r;
+}
 __device__ __forceinline__ void take_key(uint32_t key, uint32_t& K1, uint32_t& K2) {
     uint32_t md;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(md) : "v"(K1), "v"(K2), "v"(key));
@@ -375,8 +416,8 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         for (int k = 0; k < NQ; ++k) {
             const float4 pp = *reinterpret_cast<const float4*>(candf + ws[k] * kSub + t);
             const f32x2v d = screen_pair(pp, qx[k], qy[k]);
-            take_key((__float_as_uint(d.x) & ~kWinLow) | static_cast<uint32_t>(t), K1[k], K2[k]);
-            take_key((__float_as_uint(d.y) & ~kWinLow) | static_cast<uint32_t>(t + 1), K1[k], K2[k]);
+            take_key(and_or(__float_as_uint(d.x), ~kWinLow, static_cast<uint32_t>(t)), K1[k], K2[k]);
+            take_key(and_or(__float_as_uint(d.y), ~kWinLow, static_cast<uint32_t>(t + 1)), K1[k], K2[k]);
         }
     }
 #pragma unroll
@@ -416,7 +457,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             const float4 b1 = box8[min(max(c1, 0), nsub - 1)];
             float lb = box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, b0);
             if (sh * sh > 1) lb = fminf(lb, box_lb(f32x2{qx[k], qy[k]}, f32x2{qx[k], qy[k]}, b1));
-            rl = fminf(rl, sqrtf(lb) * (1.0f - 1e-5f));
+            rl = fminf(rl, sqrt_bound(lb) * (1.0f - 1e-5f));
         }
         const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2[k];
 #ifdef SLAM_ABL_GROUP
@@ -451,7 +492,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         const float bx1 = wave_max_f(act[k] ? qx[k] : -INFINITY);
         const float by0 = wave_min_f(act[k] ? qy[k] : INFINITY);
         const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
-        const float gM2 = wave_max_f(act[k] ? M2[k] : -INFINITY);
+        const float gM2 = wave_max_nn(act[k] ? M2[k] : 0.0f);
         float gf = INFINITY, lmin = INFINITY;
         flap(5);
         for (int w = 0; w < nw; ++w) {
@@ -515,8 +556,8 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             }
         }
         // lb <= d32 <= (1 + 5u) |q - p|^2, so |q - p| >= sqrt(lb) (1 - 1e-5)
-        const float gfar = wave_min_f(gf);
-        if (act[k]) st[k * st_stride] = st_pack(sqrtf(fminf(gfar, lmin)) * (1.0f - 1e-5f), ws[k]);
+        const float gfar = wave_min_nn(gf);
+        if (act[k]) st[k * st_stride] = st_pack(sqrt_bound(fminf(gfar, lmin)) * (1.0f - 1e-5f), ws[k]);
         const int na = stamping ? __popcll(__ballot(act[k])) : 0;
         if (stamping && lane == 0) {
             // diagnostics: per active-lane bucket (1, 2-4, 5-8, 9-16, 17-32, 33-64): group
@@ -538,7 +579,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
 // T > d1: the winner (exact distance d1) is the unique exact minimum.  Fc is
 // an upper bound of F(d1) (sqrt rounded up through fp32, 1e-12 relative slack).
 __device__ __forceinline__ bool certify(double d1, double s2, double a) {
-    const float sq = sqrtf(static_cast<float>(d1)) * (1.0f + 1e-6f) + 1e-19f;   // >= sqrt(d1)
+    const float sq = sqrt_bound(static_cast<float>(d1) + 1e-30f) * (1.0f + 1e-6f);   // >= sqrt(d1)
     const double fc = fma(1.0 + 8.0 * 0x1p-24, d1, fma(3.0 * a, static_cast<double>(sq), 3.0 * a * a)) *
                           (1.0 + 1e-12) + 1e-37;
     return s2 > fc;
@@ -590,6 +631,9 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
 
 // Gang exchange of one iteration's 16 exact partial sums (lane q of every wave
 // holds value q) as data-tagged granules: the data IS the flag (guide R2).
+// Exchange e is the pair's absolute ICP iteration, so the tags of a pair that
+// resumes in a later scheduler phase never match a granule left by an earlier
+// phase in the same slots (no re-zeroing between phases).
 // Granule l < 32 of a part is the 8-byte {tag = e + 1, half (l >> 4) of value
 // (l & 15)}, written by ONE relaxed agent-scope (sc1) store; no drain, no
 // counter.  Every wave sweeps all parts' granules (sc1 loads, all in flight:
@@ -854,6 +898,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         return;   // uniform
     }
 
+    if (tid == 0 && part == 0) trace_mark(a, b, 0);
     const PairSetup ps = stage_pair<BLOCK, SCREEN, PRUNE>(a, n1, n2, p1, p2, resident, cand, candf, box8, red0, red1,
                                                           pconst);
     const double cmax = ps.cmax;
@@ -954,7 +999,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         const float xf = static_cast<float>(x), yf = static_cast<float>(y);
                         const float ex = fmaf(dT[1], yf, fmaf(dT[0], xf, dT[2]));
                         const float ey = fmaf(dT[4], yf, fmaf(dT[3], xf, dT[5]));
-                        const float dl = (sqrtf(fmaf(ey, ey, ex * ex)) +
+                        const float dl = (sqrt_bound(fmaf(ey, ey, ex * ex)) +
                                           1e-6f * (fabsf(fx[k]) + fabsf(fy[k]) + fabsf(ex) + fabsf(ey)) + dsig) *
                                          (1.0f + 1e-5f);
                         const uint32_t so = qst[k * BLOCK + tid];
@@ -1183,7 +1228,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             // a partner that never arrived: stop at once, write nothing (the
             // repair launch re-runs the pair from its phase-1 state)
             if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
-                                            parts, it - it0, a.gang_wait, pconst + kBcast))
+                                            parts, it, a.gang_wait, pconst + kBcast))
                 return;
         }
         const double n = static_cast<double>(n1);
@@ -1270,6 +1315,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
                     a.out_iters[b] = it + 1;
+                    trace_mark(a, b, 1);
                 }
                 return;
             }
@@ -1283,6 +1329,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     a.out_err[b] = err;
                     a.out_iters[b] = -(it + 1);
                     a.sched_key[b] = static_cast<float>(derr);
+                    trace_mark(a, b, 1);
                 }
                 return;
             }
@@ -1415,7 +1462,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
             const float xf = static_cast<float>(x), yf = static_cast<float>(y);
             const float ex = fmaf(dT[1], yf, fmaf(dT[0], xf, dT[2]));
             const float ey = fmaf(dT[4], yf, fmaf(dT[3], xf, dT[5]));
-            const float dl = (sqrtf(fmaf(ey, ey, ex * ex)) + 1e-6f * (fabsf(fx) + fabsf(fy) + fabsf(ex) + fabsf(ey)) +
+            const float dl = (sqrt_bound(fmaf(ey, ey, ex * ex)) + 1e-6f * (fabsf(fx) + fabsf(fy) + fabsf(ex) + fabsf(ey)) +
                               dsig) * (1.0f + 1e-5f);
             st = st_pack((st_radius(st) - dl) * (1.0f - 1e-5f), st_ws(st));
         }
@@ -1467,7 +1514,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
                     const float4 b1 = box8[min(max(c1, 0), nsub - 1)];
                     float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, b0);
                     if (sh * sh > 1) lb = fminf(lb, box_lb(f32x2{fx, fy}, f32x2{fx, fy}, b1));
-                    rl = fminf(rl, sqrtf(lb) * (1.0f - 1e-5f));
+                    rl = fminf(rl, sqrt_bound(lb) * (1.0f - 1e-5f));
                 }
                 const bool settled = sh * sh <= 4 && rl * rl * (1.0f - 1e-5f) > M2;
                 act = valid && !settled;
@@ -1482,7 +1529,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
                 const float bx1 = wave_max_f(act ? fx : -INFINITY);
                 const float by0 = wave_min_f(act ? fy : INFINITY);
                 const float by1 = wave_max_f(act ? fy : -INFINITY);
-                const float gM2 = wave_max_f(act ? M2 : -INFINITY);
+                const float gM2 = wave_max_nn(act ? M2 : 0.0f);
                 float gf = INFINITY;
                 int bcount = 0;
                 for (int w = 0; w < nw; ++w) {
@@ -1536,7 +1583,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
                         }
                     }
                 }
-                gfar = wave_min_f(gf);
+                gfar = wave_min_nn(gf);
             }
             // merge the team's extra candidates (disjoint from the window and from
             // each other) and the clearance bounds
@@ -1556,7 +1603,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
                            __uint_as_float(xb2[(w * 4 + 2) * 64 + lane]), static_cast<int>(xb2[(w * 4 + 1) * 64 + lane]));
                 lm = fminf(lm, __uint_as_float(xb2[(w * 4 + 3) * 64 + lane]));
             }
-            if (act) st = st_pack(sqrtf(fminf(gfar, lm)) * (1.0f - 1e-5f), ws);
+            if (act) st = st_pack(sqrt_bound(fminf(gfar, lm)) * (1.0f - 1e-5f), ws);
         }
         tstamp(5);
         // certification (identical in every wave) and the exact fallback
@@ -1631,7 +1678,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
             tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
             tstamp(7);
             if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
-                                            parts, it - it0, a.gang_wait, pconst + kBcast)) {
+                                            parts, it, a.gang_wait, pconst + kBcast)) {
                 tflush();
                 return;   // a partner timed out: nothing written, the repair launch re-runs the pair
             }
@@ -1710,6 +1757,366 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Wide tier (latency mode for the few slowest pairs of a small batch).  A pair
+// runs on one workgroup per 64-query group (as the team kernel), but the NN
+// search is a plain BRUTE-FORCE fp32 screen split over the workgroup's NW
+// waves by candidate slices — no window, no clearance, no visit loop: a
+// group's cost is the same whatever its queries, so no outlier group sets the
+// iteration.  Per iteration:
+//   all waves  transform the group's 64 queries, scan their chunks of 32
+//              candidates keeping chunk minima (M1, its chunk, M2 over chunks),
+//              publish them in LDS (barrier);
+//   wave 0     merges the NW partial results in candidate order, rescans the
+//              winning chunk (exact index, in-chunk runner-up), certifies in
+//              fp64 (the exact scan for the rest, as every kernel), forms the
+//              exact grid sums (wave_sum_exact16), exchanges them with the
+//              other groups' workgroups (tagged granules), applies the Kabsch
+//              update and the stopping rules, and publishes T (barrier).
+// The search result is the full screen's (M1 / J1 / runner-up as mode 1), the
+// certified match the exact fp64 argmin and the sums exact on fixed grids:
+// results equal every other kernel bit for bit.
+// ---------------------------------------------------------------------------
+#ifndef SLAM_WIDE_WAVES
+#define SLAM_WIDE_WAVES 8
+#endif
+constexpr int kWideWaves = SLAM_WIDE_WAVES;
+constexpr int kWideBlock = 64 * kWideWaves;
+__host__ __device__ constexpr size_t wide_lds_bytes(int cap) {
+    return red_doubles(kWideBlock) * sizeof(double) + static_cast<size_t>(cap) * (sizeof(double2) + sizeof(float2)) +
+           static_cast<size_t>(kWideWaves) * 3 * 64 * sizeof(uint32_t) + 8 * sizeof(double);
+}
+
+// src/icp.py:22-46 + 64-67 from the 16 exact partial sums (lane q holds value
+// q, every lane the same T): the Kabsch update of icp_kernel, one wave.
+struct KabschOut {
+    SE2 Tn;
+    double err;
+};
+__device__ __forceinline__ KabschOut kabsch_from_sums(double tot, const SE2& T, const double* pconst, int n1,
+                                                      bool rotation_only) {
+    const double n = static_cast<double>(n1);
+    const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
+    const double mvy = (readlane_d(tot, 2) + readlane_d(tot, 3)) / n;
+    KabschOut o;
+    o.err = readlane_d(tot, 4) + readlane_d(tot, 5);
+    const double2 dp = *reinterpret_cast<const double2*>(pconst + kDpX);
+    const double2 mup = *reinterpret_cast<const double2*>(pconst + kMupX);
+    const double mux = fma(T.m02, 1.0, fma(T.m01, mup.y, T.m00 * mup.x));   // pc1_avg = T mu_p
+    const double muy = fma(T.m12, 1.0, fma(T.m11, mup.y, T.m10 * mup.x));
+    const double p00 = fma(-dp.x, mvx, readlane_d(tot, 6) + readlane_d(tot, 7));
+    const double p01 = fma(-dp.x, mvy, readlane_d(tot, 8) + readlane_d(tot, 9));
+    const double p10 = fma(-dp.y, mvx, readlane_d(tot, 10) + readlane_d(tot, 11));
+    const double p11 = fma(-dp.y, mvy, readlane_d(tot, 12) + readlane_d(tot, 13));
+    const double s00 = fma(T.m01, p10, T.m00 * p00);
+    const double s01 = fma(T.m01, p11, T.m00 * p01);
+    const double s10 = fma(T.m11, p10, T.m10 * p00);
+    const double s11 = fma(T.m11, p11, T.m10 * p01);
+    const double cs = s00 + s11;
+    const double sn = s01 - s10;
+    const double r = sqrt(cs * cs + sn * sn);
+    const double co = r > 0.0 ? cs / r : 1.0;
+    const double si = r > 0.0 ? sn / r : 0.0;
+    double tx = mvx - fma(-si, muy, co * mux);
+    double ty = mvy - fma(co, muy, si * mux);
+    if (rotation_only) {
+        tx = 0.0;
+        ty = 0.0;
+    }
+    SE2 D;
+    D.m00 = co; D.m01 = -si; D.m02 = tx;
+    D.m10 = si; D.m11 = co;  D.m12 = ty;
+    o.Tn = se2_mul(D, T);
+    return o;
+}
+
+// The wide pairs' fp32 candidates in the pair layout of candf (cf_put), one
+// `cap` slab per wide slot, in global memory: the wide kernel streams them
+// through SCALAR loads (s_load_dwordx16: 8 candidates into SGPRs, uniform for
+// the wave) instead of LDS broadcasts (1 KB to VGPRs per ds_read_b128).
+__global__ __launch_bounds__(256) void wide_prep_kernel(IcpArgs a, float2* __restrict__ wcand) {
+    const int slot = blockIdx.x;
+    if (slot >= a.n_gangs) return;
+    const int b = a.order ? a.order[slot] : slot;
+    const int s2 = a.dst_scan[b];
+    const int64_t o2 = a.scan_off[s2];
+    const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
+    float2* dst = wcand + static_cast<int64_t>(slot) * a.cand_cap;
+    for (int j = threadIdx.x; j < a.cand_cap; j += 256) {
+        float x = kSentinel, y = kSentinel;
+        if (j < n2) {
+            const double2 p = a.pts[o2 + j];
+            x = static_cast<float>(p.x);
+            y = static_cast<float>(p.y);
+        }
+        cf_put(dst, j, x, y);
+    }
+}
+
+__global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const float4* __restrict__ wcand) {
+    constexpr int NW = kWideWaves;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* red0 = reinterpret_cast<double*>(smem);
+    double* red1 = red0 + NW * 16;
+    double* pconst = red0 + 2 * NW * 16;
+    double2* cand = reinterpret_cast<double2*>(smem + red_doubles(kWideBlock) * sizeof(double));
+    const int cap = a.cand_cap;
+    float2* candf = reinterpret_cast<float2*>(cand + cap);
+    uint32_t* xs = reinterpret_cast<uint32_t*>(candf + cap);    // [NW][3][64]: M1, chunk, M2 per wave
+    double* tb = reinterpret_cast<double*>(xs + NW * 3 * 64);   // the next T (6) and the flag
+
+    const int parts = a.gang;
+    const int bx = static_cast<int>(blockIdx.x);
+    const int slot = (bx / (8 * parts)) * 8 + (bx & 7);   // a pair's workgroups on one XCD
+    const int part = (bx >> 3) % parts;                     // = its 64-query group
+    if (slot >= a.n_gangs) return;
+    const int b = a.order ? a.order[slot] : slot;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int it0 = 0;
+    if (a.resume) {
+        const int s = a.out_iters[b];
+        if (s > 0 || s == kBadBounds) return;
+        it0 = -s;
+    }
+    const int s1 = a.src_scan[b], s2 = a.dst_scan[b];
+    const int64_t o1 = a.scan_off[s1], o2 = a.scan_off[s2];
+    const int n1 = static_cast<int>(a.scan_off[s1 + 1] - o1);
+    const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
+    const double2* __restrict__ p1 = a.pts + o1;
+    const double2* __restrict__ p2 = a.pts + o2;
+    if (n1 < 1 || n2 < 1 || n1 > 64 * parts || n2 > cap) {
+        if (tid == 0 && part == 0) {
+            a.out_iters[b] = kBadBounds;
+            a.out_err[b] = __builtin_nan("");
+            atomicOr(&g_icp_status, 1);
+        }
+        return;
+    }
+    if (tid == 0 && part == 0) trace_mark(a, b, 0);
+    const PairSetup ps = stage_pair<kWideBlock, true, false>(a, n1, n2, p1, p2, true, cand, candf, nullptr, red0,
+                                                             red1, pconst);
+    SE2 T = load_se2((it0 > 0 ? a.out_tf : a.init) + 9 * static_cast<int64_t>(b));
+    if (a.rotation_only) {
+        T.m02 = 0.0;
+        T.m12 = 0.0;
+    }
+    double* hist = a.hist_stride > 0 ? a.out_hist + static_cast<int64_t>(b) * a.hist_stride * 9 : nullptr;
+    if (hist && tid == 0 && part == 0 && it0 == 0) store_se2(hist, T);
+    double last_err = it0 > 0 ? a.out_err[b] : 0.0;
+    const int i = part * 64 + lane;
+    const bool valid = i < n1;
+    const int nch = (n2 + kChunk - 1) / kChunk;
+    const int c_lo = wave * nch / NW, c_hi = (wave + 1) * nch / NW;   // this wave's chunks
+    uint64_t* slots = a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32;
+    // diagnostics (a.stamps != NULL): s_memtime per phase of wave 0 of every
+    // part, stamps[256 + 16 * part + phase] (tools/wide_stamps.py)
+    const bool stamping = a.stamps != nullptr && wave == 0;
+    unsigned long long tp = stamping ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    auto tstamp = [&](int q) {
+        if (stamping) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            tacc[q] += t1 - tp;
+            tp = t1;
+        }
+    };
+    for (int it = it0;; ++it) {
+        double x = 0.0, y = 0.0;
+        if (valid) {
+            const double2 p = p1[i];
+            x = p.x;
+            y = p.y;
+        }
+        const double qx = fma(T.m02, 1.0, fma(T.m01, y, T.m00 * x));
+        const double qy = fma(T.m12, 1.0, fma(T.m11, y, T.m10 * x));
+        const float fx = static_cast<float>(qx), fy = static_cast<float>(qy);
+        // ---- this wave's slice: chunk minima (screened distances are >= 0:
+        //      their bits order as unsigned integers) ---------------------------
+        uint32_t M1 = 0xffffffffu, M2 = 0xffffffffu;
+        int C1 = 0;
+        if (ps.screen) {
+            const float4* __restrict__ cg = wcand + static_cast<int64_t>(slot) * (cap / 2);   // uniform: s_load
+            for (int c = c_lo; c < c_hi; ++c) {
+                const float4* cp = cg + c * (kChunk / 2);
+                uint32_t cm = 0xffffffffu;
+#pragma unroll
+                for (int t = 0; t < kChunk / 2; ++t) {
+                    const f32x2v d = screen_pair(cp[t], fx, fy);
+                    cm = min(cm, min(__float_as_uint(d.x), __float_as_uint(d.y)));   // v_min3_u32
+                }
+                C1 = cm < M1 ? c : C1;
+                uint32_t md;
+                asm("v_med3_u32 %0, %1, %2, %3" : "=v"(md) : "v"(M1), "v"(M2), "v"(cm));
+                M2 = md;
+                M1 = min(M1, cm);
+            }
+        }
+        tstamp(0);
+        xs[(wave * 3 + 0) * 64 + lane] = M1;
+        xs[(wave * 3 + 1) * 64 + lane] = static_cast<uint32_t>(C1);
+        xs[(wave * 3 + 2) * 64 + lane] = M2;
+        __syncthreads();
+        tstamp(1);
+        if (wave == 0) {
+            // merge in candidate (wave) order: strict < keeps the first chunk on ties
+            uint32_t m1 = 0xffffffffu, m2 = 0xffffffffu;
+            int c1 = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t a1 = xs[(w * 3 + 0) * 64 + lane], a2 = xs[(w * 3 + 2) * 64 + lane];
+                const int ac = static_cast<int>(xs[(w * 3 + 1) * 64 + lane]);
+                c1 = a1 < m1 ? ac : c1;
+                m2 = min(max(m1, a1), min(m2, a2));
+                m1 = min(m1, a1);
+            }
+            // the winning chunk: first index reaching the minimum + in-chunk
+            // runner-up; its 16 candidate pairs read at once, then two
+            // independent chains (even / odd pairs) merged in index order
+            float b1 = INFINITY, b2 = INFINITY;
+            int j1 = c1 * kChunk;
+            {
+                const float4* cp = reinterpret_cast<const float4*>(candf + c1 * kChunk);
+                float4 pp[kChunk / 2];
+#pragma unroll
+                for (int t = 0; t < kChunk / 2; ++t) pp[t] = cp[t];
+                float e1[2] = {INFINITY, INFINITY}, e2[2] = {INFINITY, INFINITY};
+                int ej[2] = {0, 0};
+#pragma unroll
+                for (int t = 0; t < kChunk / 2; ++t) {
+                    const f32x2v d = screen_pair(pp[t], fx, fy);
+                    const int h = t & 1;
+                    take_cand(d.x, 2 * t, e1[h], e2[h], ej[h]);
+                    take_cand(d.y, 2 * t + 1, e1[h], e2[h], ej[h]);
+                }
+                // chain 0 holds offsets {0,1,4,5,...}, chain 1 {2,3,6,7,...}: on a tie
+                // the smaller offset wins (the full scan's first index)
+                const bool one = e1[1] < e1[0] || (e1[1] == e1[0] && ej[1] < ej[0]);
+                b1 = one ? e1[1] : e1[0];
+                j1 += one ? ej[1] : ej[0];
+                b2 = fminf(fmaxf(e1[0], e1[1]), fminf(e2[0], e2[1]));
+            }
+            j1 = min(j1, n2 - 1);
+            int bi = j1;
+            tstamp(2);
+            const double2 cw = cand[j1];
+            double dq = exact_d2(cw.x, cw.y, qx, qy);
+            bool ok = true;
+            if (!ps.screen) {
+                ok = !valid;
+            } else if (valid && n2 > 1) {
+                const double s2 = static_cast<double>(fminf(__uint_as_float(m2), b2));
+                const double cq = fmax(fabs(qx), fabs(qy));
+                const double ab = (1.0 + 0x1p-24) * 0x1p-24 * (ps.cmax + cq);
+                ok = cq < 1e18 && s2 < 3.0e38 && certify(dq, s2, ab);
+            }
+            uint64_t fails = __ballot(!ok);
+            while (fails) {   // the exact fp64 scan for each uncertified query (first index on ties)
+                const int src = static_cast<int>(__builtin_ctzll(fails));
+                fails &= fails - 1;
+                const double xs_ = bcast_d(qx, src), ys_ = bcast_d(qy, src);
+                double bd = INFINITY;
+                int bj = lane < n2 ? lane : 0x7fffffff;
+                for (int j = lane; j < n2; j += 64) {
+                    const double2 c = cand[j];
+                    const double d = exact_d2(c.x, c.y, xs_, ys_);
+                    if (d < bd) {
+                        bd = d;
+                        bj = j;
+                    }
+                }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const double od = __shfl_xor(bd, off, 64);
+                    const int oj = __shfl_xor(bj, off, 64);
+                    if (od < bd || (od == bd && oj < bj)) {
+                        bd = od;
+                        bj = oj;
+                    }
+                }
+                if (lane == src) {
+                    bi = bj;
+                    dq = bd;
+                }
+            }
+            tstamp(3);
+            // sums (as icp_kernel step 4), this group's 64 queries
+            const double2 c = *reinterpret_cast<const double2*>(pconst + kPcX);
+            const double2 gmv = *reinterpret_cast<const double2*>(pconst + kGm1);
+            const double2 gsv = *reinterpret_cast<const double2*>(pconst + kGs1);
+            const double2 pcm = *reinterpret_cast<const double2*>(pconst + kPmax);
+            const double bq = (fmax(fabs(T.m00) + fabs(T.m01), fabs(T.m10) + fabs(T.m11)) * pcm.x +
+                               fmax(fabs(T.m02), fabs(T.m12))) * (1.0 + 1e-12);
+            const RsumGrid gm{gmv.x, gmv.y}, gs{gsv.x, gsv.y};
+            const RsumGrid gd = rsum_grid(2.0 * (bq + pcm.y) * (bq + pcm.y) * (1.0 + 1e-12), n1);
+            double acc[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+            if (valid) {
+                const double2 m = cand[bi];
+                rsum_add(m.x, gm, acc[0], acc[1]);
+                rsum_add(m.y, gm, acc[2], acc[3]);
+                rsum_add(dq, gd, acc[4], acc[5]);
+                const double ax = x - c.x, ay = y - c.y;
+                rsum_add(ax * m.x, gs, acc[6], acc[7]);
+                rsum_add(ax * m.y, gs, acc[8], acc[9]);
+                rsum_add(ay * m.x, gs, acc[10], acc[11]);
+                rsum_add(ay * m.y, gs, acc[12], acc[13]);
+            }
+            double tot = wave_sum_exact16(acc);
+            tstamp(4);
+            bool arrived = true;
+            if (parts > 1) tot = gang_exchange_wave(tot, slots, part, parts, it, a.gang_wait, arrived);
+            tstamp(5);
+            double flag = 0.0;
+            if (!arrived) {
+                flag = 3.0;   // a partner timed out: write nothing, the repair launch re-runs the pair
+            } else {
+                const KabschOut ko = kabsch_from_sums(tot, T, pconst, n1, a.rotation_only != 0);
+                const SE2& Tn = ko.Tn;
+                const double err = ko.err;
+                if (hist && lane == 0 && part == 0) store_se2(hist + 9 * (it + 1), Tn);
+                const double derr = fabs(last_err - err);
+                const bool stop = (err < a.epsilon) || (it > a.max_iters) || (it > 0 && derr < a.stopping_thresh);
+                last_err = err;
+                if (stop) {
+                    flag = 1.0;
+                    if (lane == 0 && part == 0) {
+                        store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                        a.out_err[b] = err;
+                        a.out_iters[b] = it + 1;
+                        trace_mark(a, b, 1);
+                    }
+                } else if (a.phase_cap > 0 && it + 1 - it0 >= a.phase_cap) {
+                    flag = 2.0;
+                    if (lane == 0 && part == 0) {
+                        store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
+                        a.out_err[b] = err;
+                        a.out_iters[b] = -(it + 1);
+                        a.sched_key[b] = static_cast<float>(derr);
+                        trace_mark(a, b, 1);
+                    }
+                }
+                if (lane == 0) {
+                    tb[0] = Tn.m00; tb[1] = Tn.m01; tb[2] = Tn.m02;
+                    tb[3] = Tn.m10; tb[4] = Tn.m11; tb[5] = Tn.m12;
+                }
+            }
+            if (lane == 0) tb[6] = flag;
+            tstamp(6);
+        }
+        __syncthreads();
+        tstamp(7);
+        if (tb[6] != 0.0) {   // uniform: stop, pause or a lost partner
+            if (stamping && lane == 0)
+                for (int q = 0; q < 8; ++q) atomicAdd(a.stamps + 256 + 16 * part + q, tacc[q]);
+            return;
+        }
+        T.m00 = uniform_d(tb[0]); T.m01 = uniform_d(tb[1]); T.m02 = uniform_d(tb[2]);
+        T.m10 = uniform_d(tb[3]); T.m11 = uniform_d(tb[4]); T.m12 = uniform_d(tb[5]);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Instance table.  A (BLOCK, QPT) instance holds BLOCK*QPT queries in
 // registers; the host picks the smallest capacity >= max_n1 so idle lanes stay
 // few (1081-point scans: 64x17 = 1088 -> 99.4 % of lanes busy).
@@ -1772,6 +2179,34 @@ static const GangInstance kGangInstances[] = {
     {384, icp_kernel<384, 1, false, true, true, 1, false, true>},
     {512, icp_kernel<512, 1, false, true, true, 1, false, true>},
 };
+
+// Bulk gangs (small batches): every pair of a phase as a gang of 2 or 3
+// workgroups with the ordinary LDS footprint (4-5 workgroups per CU), so a
+// pair's iteration latency halves while the batch cannot fill the GPU with
+// whole pairs.  Several query groups per wave as the
+// bulk instances; 1081-point scans: 17 groups -> 9 per part (192x3) or 6
+// (128x3).
+struct BulkGangInstance {
+    int parts;
+    int block;
+    int qpt;
+    KernelFn fn;
+};
+static const BulkGangInstance kBulkGangInstances[] = {
+    {2, 192, 3, icp_kernel<192, 3, false, true, true, kWpe, false, true>},
+    {2, 256, 3, icp_kernel<256, 3, false, true, true, kWpe, false, true>},
+    {3, 128, 3, icp_kernel<128, 3, false, true, true, kWpe, false, true>},
+    {3, 192, 2, icp_kernel<192, 2, false, true, true, kWpe, false, true>},
+};
+static const BulkGangInstance* pick_bulk_gang_instance(int max_n1, int parts) {
+    const int groups = (max_n1 + 63) / 64;
+    const int per = (groups + parts - 1) / parts;
+    const BulkGangInstance* best = nullptr;
+    for (const BulkGangInstance& g : kBulkGangInstances)
+        if (g.parts == parts && g.block / 64 * g.qpt >= per && (!best || g.block * g.qpt < best->block * best->qpt))
+            best = &g;
+    return best;
+}
 
 // the smallest gang instance holding ceil(groups / parts) groups, or NULL
 static const GangInstance* pick_gang_instance(int max_n1, int parts) {
@@ -1852,6 +2287,7 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
 static int g_screen = 2;
 static unsigned long long* g_icp_stamps = nullptr;
 static unsigned long long* g_icp_evals = nullptr;
+static unsigned long long* g_icp_trace = nullptr;
 
 // inst_override / lds_min: the scheduler's CU-exclusive head launch (below)
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
@@ -1931,11 +2367,20 @@ static const Instance* pick_head_instance(int max_n1) {
 static int g_sched_gangs = 24;
 static int g_sched_gang_parts = 4;
 static uint32_t g_gang_wait = kGangWaitTicks;   // diagnostics can shorten it to force timeouts
+// Wide tier: the top g_sched_wide keyed pairs of a batch below kHeadsMaxPairs
+// run on icp_wide_kernel, one workgroup per 64-query group, each requesting
+// kMaxLds / g_wide_share of LDS (1: CU-exclusive)
+static int g_sched_wide = 0;
+static int g_wide_share = 1;
+// Bulk gangs: batches of fewer than g_bulk_gang_below pairs run both phases'
+// bulk as gangs of g_bulk_gang_parts workgroups (0 / 1 parts: off)
+static int g_bulk_gang_below = 0;
+static int g_bulk_gang_parts = 2;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
-    hipStream_t stream = nullptr, stream2 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr, join3 = nullptr;
 };
 static SideStream* side_stream(int dev) {
     static SideStream side[64];
@@ -1944,9 +2389,11 @@ static SideStream* side_stream(int dev) {
     if (!e.stream) {
         if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&e.stream2, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&e.stream3, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e.join2, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e.join2, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.join3, hipEventDisableTiming) != hipSuccess) {
             e.stream = nullptr;
             return nullptr;
         }
@@ -2001,6 +2448,55 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
     const int blocks = (G + 7) / 8 * 8 * parts;
     hipLaunchKernelGGL(gi->fn, dim3(blocks), dim3(gi->block), lds, s, a);
     return check_launch("icp gang kernel");
+}
+
+// B pairs (args.order, or identity) as bulk gangs (instance `bg`), slots:
+// B x 2 x parts x 32 granules, zeroed once per batch.
+static int launch_bulk_gangs(const IcpArgs& args, int B, const BulkGangInstance* bg, int max_n2, hipStream_t s,
+                             uint64_t* slots) {
+    if (B <= 0) return ok();
+    IcpArgs a = args;
+    a.stamps = nullptr;
+    a.evals = nullptr;
+    a.cand_cap = ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk;
+    a.gang = bg->parts;
+    a.n_gangs = B;
+    a.gang_slots = slots;
+    a.gang_wait = g_gang_wait;
+    const size_t lds = red_doubles(bg->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2) +
+                       static_cast<size_t>(a.cand_cap) * sizeof(float2) +
+                       static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
+                       static_cast<size_t>(bg->block) * bg->qpt * 2 * sizeof(int32_t);
+    if (lds > kMaxLds) return fail(SLAM_EINVAL, "icp bulk gangs: LDS");
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bg->fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds));
+    hipLaunchKernelGGL(bg->fn, dim3((B + 7) / 8 * 8 * bg->parts), dim3(bg->block), lds, s, a);
+    return check_launch("icp bulk gang kernel");
+}
+
+// W pairs (args.order[0..W)) on the wide tier: one workgroup per 64-query
+// group, the parts of a pair on one XCD (slots as launch_gangs).
+static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipStream_t s, uint64_t* slots,
+                       float2* wcand) {
+    const int parts = (max_n1 + 63) / 64;
+    if (max_n2 > kCandCap || parts < 1 || parts > kTeamMaxParts) return fail(SLAM_EINVAL, "icp wide tier: shape");
+    IcpArgs a = args;
+    a.stamps = g_icp_stamps;   // diagnostics: per-part phase cycles (icp_wide_kernel)
+    a.evals = nullptr;
+    a.cand_cap = ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk;
+    a.gang = parts;
+    a.n_gangs = W;
+    a.gang_slots = slots;
+    a.gang_wait = g_gang_wait;
+    const size_t need = wide_lds_bytes(a.cand_cap);
+    if (need > kMaxLds) return fail(SLAM_EINVAL, "icp wide tier: LDS");
+    const size_t lds = max(need, kMaxLds / static_cast<size_t>(max(g_wide_share, 1)));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(icp_wide_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds));
+    hipLaunchKernelGGL(wide_prep_kernel, dim3(W), dim3(256), 0, s, a, wcand);
+    hipLaunchKernelGGL(icp_wide_kernel, dim3((W + 7) / 8 * 8 * parts), dim3(kWideBlock), lds, s, a,
+                       reinterpret_cast<const float4*>(wcand));
+    return check_launch("icp wide kernel");
 }
 
 // Stable counting sort of the pairs by bucket, so order[] (which pairs become
@@ -2118,12 +2614,27 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const int parts = team ? (max_n1 + 63) / 64 : g_sched_gang_parts;
     const bool gang_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap &&
                          (team ? parts <= kTeamMaxParts : parts >= 2 && pick_gang_instance(max_n1, parts) != nullptr);
-    const int G = gang_ok ? min(g_sched_gangs, heads) : 0;
-    const size_t gang_slot_bytes = static_cast<size_t>(G) * 2 * max(parts, 1) * 32 * sizeof(uint64_t);
+    // tiers of phase 2: wide (order[0, Wd)), gangs (order[Wd, Wd + G)), heads, bulk
+    const int wide_parts = (max_n1 + 63) / 64;
+    const bool wide_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap && wide_parts <= kTeamMaxParts &&
+                         wide_lds_bytes(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) <= kMaxLds;
+    const int Wd = wide_ok ? min(g_sched_wide, heads) : 0;
+    const int G = gang_ok ? max(0, min(g_sched_gangs, heads - Wd)) : 0;
+    const size_t wide_slot_words = static_cast<size_t>(Wd) * 2 * wide_parts * 32;
+    const size_t gang_slot_bytes =
+        (static_cast<size_t>(G) * 2 * max(parts, 1) * 32 + wide_slot_words) * sizeof(uint64_t);
+    const size_t wide_cand_bytes = static_cast<size_t>(Wd) * ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk *
+                                   sizeof(float2);
+    // bulk gangs for a batch too small to fill the GPU with whole pairs
+    const BulkGangInstance* bg =
+        B < g_bulk_gang_below && g_bulk_gang_parts >= 2 && g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap
+            ? pick_bulk_gang_instance(max_n1, g_bulk_gang_parts)
+            : nullptr;
+    const size_t bulk_slot_bytes = bg ? nb * 2 * bg->parts * 32 * sizeof(uint64_t) : 0;
     const int nblk = (B + kSortBlock - 1) / kSortBlock;
     const size_t sched_bytes =
         (static_cast<size_t>(nblk) * kNB * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float)) + 255) / 256 * 256;
-    const size_t bytes = sched_bytes + gang_slot_bytes;
+    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);   // hist_blk[nblk][kNB]
@@ -2131,13 +2642,28 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     int32_t* order = bucket + nb;
     float* key = reinterpret_cast<float*>(order + nb);
     uint64_t* gang_slots = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes);
+    float2* wide_cand = reinterpret_cast<float2*>(static_cast<char*>(ws) + sched_bytes + gang_slot_bytes);
+    uint64_t* bulk_slots =
+        reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes + gang_slot_bytes + wide_cand_bytes);
     IcpArgs a = args;
     a.phase_cap = probe;
     a.sched_key = key;
-    int rc = launch(false, a, B, max_n1, max_n2, stream);
+    int rc;
+    if (bg) {
+        // a phase-1 gang that timed out writes nothing: its pair must then read
+        // as "not started" (out_iters 0) in phase 2, never as a stale result
+        (void)hipMemsetAsync(args.out_iters, 0, nb * sizeof(int32_t), s);
+        (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
+        rc = launch_bulk_gangs(a, B, bg, max_n2, s, bulk_slots);
+    } else {
+        rc = launch(false, a, B, max_n1, max_n2, stream);
+    }
     if (rc == 0) {
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
-        if (G > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
+        if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
+        // phase 2 gives pairs new slots: clear phase 1's granules (a pair restarted
+        // from iteration 0 would otherwise meet another pair's old tags)
+        if (bg) (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
         hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr, hist,
                            bucket);
         hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
@@ -2148,43 +2674,55 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         a.phase_cap = 0;
         a.resume = 1;
         a.order = order;
-        const Instance* hinst = heads > G && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
+        const int GW = Wd + G;   // pairs on the exchange tiers (wide, then gangs)
+        const Instance* hinst = heads > GW && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
         int dev = 0;
         SideStream* side = nullptr;
-        if ((hinst || G > 0) && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
+        if ((hinst || GW > 0 || bg) && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
         if (side) {
             // fork: the gangs and the head pairs on CU-exclusive workgroups first
             // (the GPU is empty after the scheduler kernels: they take the first
             // CUs), gangs on the caller's stream, heads on the second side stream,
             // the rest on the side stream behind the fork event, which resolves
             // after the first launches are queued; join before the workspace is freed
-            const int H = hinst ? heads : G;
+            const int H = hinst ? heads : GW;
             if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess ||
-                hipStreamWaitEvent(side->stream2, side->fork, 0) != hipSuccess)
+                hipStreamWaitEvent(side->stream2, side->fork, 0) != hipSuccess ||
+                hipStreamWaitEvent(side->stream3, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
-            if (rc == 0 && G > 0) rc = launch_gangs(a, G, parts, team, max_n1, max_n2, s, gang_slots);
-            if (rc == 0 && H > G) {
+            // the wide tier on its own stream (the gangs must not queue behind it)
+            if (rc == 0 && Wd > 0) rc = launch_wide(a, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand);
+            if (rc == 0 && G > 0) {
+                IcpArgs g = a;
+                g.order = order + Wd;
+                rc = launch_gangs(g, G, parts, team, max_n1, max_n2, s, gang_slots + wide_slot_words);
+            }
+            if (rc == 0 && H > GW) {
                 IcpArgs h = a;
-                h.order = order + G;
-                rc = launch(false, h, H - G, max_n1, max_n2, side->stream2, hinst, kMaxLds);
+                h.order = order + GW;
+                rc = launch(false, h, H - GW, max_n1, max_n2, side->stream2, hinst, kMaxLds);
             }
             IcpArgs t = a;
             t.order = order + H;
-            if (rc == 0) rc = launch(false, t, B - H, max_n1, max_n2, side->stream);
+            if (rc == 0)
+                rc = bg ? launch_bulk_gangs(t, B - H, bg, max_n2, side->stream, bulk_slots + static_cast<size_t>(H) * 2 * bg->parts * 32)
+                        : launch(false, t, B - H, max_n1, max_n2, side->stream);
             if (rc == 0 && (hipEventRecord(side->join, side->stream) != hipSuccess ||
-                            hipEventRecord(side->join2, side->stream2) != hipSuccess))
+                            hipEventRecord(side->join2, side->stream2) != hipSuccess ||
+                            hipEventRecord(side->join3, side->stream3) != hipSuccess))
                 rc = fail(SLAM_EHIP, "icp scheduler: join");
             if (rc == 0 && (hipStreamWaitEvent(s, side->join, 0) != hipSuccess ||
-                            hipStreamWaitEvent(s, side->join2, 0) != hipSuccess))
+                            hipStreamWaitEvent(s, side->join2, 0) != hipSuccess ||
+                            hipStreamWaitEvent(s, side->join3, 0) != hipSuccess))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
-            if (rc == 0 && G > 0) {
-                // repair: a gang whose partners did not all arrive stopped without
-                // writing, leaving its pair paused at the phase-1 state; re-run
-                // such pairs on one workgroup each (finished pairs' workgroups
-                // exit at once, so this costs one near-empty launch)
+            if (rc == 0 && (GW > 0 || bg)) {
+                // repair: a wide / gang pair whose partners did not all arrive
+                // stopped without writing, leaving it paused at the phase-1 state;
+                // re-run such pairs on one workgroup each (finished pairs'
+                // workgroups exit at once, so this costs one near-empty launch)
                 IcpArgs r = a;
                 r.order = order;
-                rc = launch(false, r, G, max_n1, max_n2, stream);
+                rc = launch(false, r, bg ? B : GW, max_n1, max_n2, stream);
             }
         } else {
             rc = launch(false, a, B, max_n1, max_n2, stream);
@@ -2223,6 +2761,12 @@ int slam_icp_set_stamps(void* dev_buf) {
     g_icp_stamps = reinterpret_cast<unsigned long long*>(dev_buf);
     return ok();
 }
+// Diagnostics: per-pair phase timeline of slam_icp_batch_f64 (IcpArgs::trace):
+// a device buffer of B x 2 x 4 uint64; NULL turns it off.
+int slam_icp_set_trace(void* dev_buf) {
+    g_icp_trace = reinterpret_cast<unsigned long long*>(dev_buf);
+    return ok();
+}
 int slam_icp_set_eval_counter(void* dev_u64) {
     g_icp_evals = reinterpret_cast<unsigned long long*>(dev_u64);
     return ok();
@@ -2245,6 +2789,26 @@ int slam_icp_set_schedule_gangs(int gangs, int parts) {
 // Gang parts that timed out waiting for a partner since the last call (their
 // pairs were re-run on single workgroups: results stay valid); read-and-clear.
 // Synchronises the device.
+// Wide tier: the `pairs` slowest-keyed pairs of a batch below 8,192 pairs on
+// icp_wide_kernel (before the gangs), workgroups requesting 1/share of a CU's
+// LDS (1: CU-exclusive).  Results are bit-identical.  0 = off.
+int slam_icp_set_schedule_wide(int pairs, int share) {
+    if (pairs < 0 || share < 1 || share > 8) return fail(SLAM_EINVAL, "schedule: wide %d share %d", pairs, share);
+    g_sched_wide = pairs;
+    g_wide_share = share;
+    return ok();
+}
+// Bulk gangs: batches of fewer than `below_pairs` pairs (>= the scheduler's
+// minimum) run every phase's bulk as gangs of `parts` (2 or 3) workgroups
+// with the ordinary LDS footprint: half the iteration latency per pair when
+// whole pairs cannot fill the GPU.  Bit-identical results.  0 = off.
+int slam_icp_set_bulk_gangs(int below_pairs, int parts) {
+    if (below_pairs < 0 || (below_pairs > 0 && (parts < 2 || parts > 3)))
+        return fail(SLAM_EINVAL, "bulk gangs: below %d parts %d", below_pairs, parts);
+    g_bulk_gang_below = below_pairs;
+    g_bulk_gang_parts = parts;
+    return ok();
+}
 int slam_icp_gang_timeouts(void) {
     int v = 0;
     const int zero = 0;
@@ -2342,6 +2906,7 @@ int slam_icp_batch_f64(const double* pts, const int64_t* scan_off, const int32_t
     a.out_tf = out_tf;
     a.out_err = out_err;
     a.out_iters = out_iters;
+    a.trace = g_icp_trace;
     return launch_batch(a, B, max_n1, max_n2, stream);
 }
 

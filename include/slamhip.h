@@ -222,6 +222,19 @@ int slam_icp_set_schedule_heads(int heads);
  * bit-identical to the one-workgroup kernels.  gangs = 0: off; defaults
  * (24, 4).  SLAM_EINVAL for gangs < 0, parts 1, < 0 or > 17. */
 int slam_icp_set_schedule_gangs(int gangs, int parts);
+/* Wide tier: the `pairs` slowest-keyed pairs (taken before the gangs) run on
+ * one workgroup per 64-query group (pairs up to 2,048 points) whose NW waves
+ * split a brute-force fp32 screen by candidate slices (no pruning, so no
+ * outlier group sets the iteration time); the groups exchange their exact
+ * partial sums every iteration like the gangs.  Workgroups request 1/share of
+ * a CU's LDS (1: CU-exclusive).  Bit-identical results; 0 = off. */
+int slam_icp_set_schedule_wide(int pairs, int share);
+/* Bulk gangs: batches of fewer than `below_pairs` pairs run the bulk of both
+ * scheduler phases as gangs of `parts` (2 or 3) workgroups with the ordinary
+ * LDS footprint — half (a third) of a pair's iteration latency when whole
+ * pairs cannot fill the GPU (strong-scaling shards).  Bit-identical results.
+ * below_pairs = 0: off. */
+int slam_icp_set_bulk_gangs(int below_pairs, int parts);
 /* Gang parts that waited longer than the gang wait (default 0.2 s) for a
  * partner since the last call (read-and-clear; synchronises the device).  Such
  * a part stops at once without writing; after phase 2 the scheduler re-runs
@@ -253,6 +266,11 @@ int slam_icp_set_stamps(void* dev_buf);
  * counter run in a separate diagnostics build of the pruned batch kernel
  * (NN mode 2, slam_icp_batch_f64 only); the product kernels carry neither. */
 int slam_icp_set_eval_counter(void* dev_u64);
+/* Diagnostics: the per-pair phase timeline of slam_icp_batch_f64 into a device
+ * buffer of B x 2 x 4 uint64 — per pair and scheduler phase the
+ * s_memrealtime (100 MHz) at which its workgroup (part 0) started and ended
+ * and where it ran (XCC << 32 | HW_ID); NULL turns it off. */
+int slam_icp_set_trace(void* dev_buf);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,9 @@ from conftest import case_arrays, homog
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-9
+DEFAULT_GANGS = (24, 4)   # the library's scheduler defaults (restored after a test changes them)
+DEFAULT_WIDE = (0, 1)
+DEFAULT_BULK = (0, 2)
 
 
 @pytest.fixture(scope="module")
@@ -436,6 +439,21 @@ def test_gangs_are_bit_identical(k):
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
             runs[(gangs, parts)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() == 0
+        # the wide tier (brute-force screen over candidate slices), alone and before gangs
+        for wide, share, gangs in ((64, 1, 0), (8, 2, 16), (3, 4, 24)):
+            assert lib.slam_icp_set_schedule_gangs(gangs, 4) == 0
+            assert lib.slam_icp_set_schedule_wide(wide, share) == 0
+            runs[("wide", wide, share, gangs)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100,
+                                                             history=True)
+            assert lib.slam_icp_gang_timeouts() == 0
+        assert lib.slam_icp_set_schedule_wide(0, 1) == 0
+        # bulk gangs: both phases' bulk as gangs of 2 / 3 ordinary workgroups
+        for parts in (2, 3):
+            assert lib.slam_icp_set_bulk_gangs(4096, parts) == 0
+            assert lib.slam_icp_set_schedule_gangs(24, 4) == 0
+            runs[("bulk", parts)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+            assert lib.slam_icp_gang_timeouts() == 0
+        assert lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK) == 0
         assert lib.slam_icp_set_schedule_gangs(64, 4) == 0   # rotation-only, max_iters stop inside phase 2
         ro = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=7, rotation_only=True)
         assert lib.slam_icp_set_schedule(0, 1024) == 0
@@ -443,7 +461,9 @@ def test_gangs_are_bit_identical(k):
         assert lib.slam_icp_set_schedule_gangs(1, 1) != 0   # a gang needs two parts
     finally:
         lib.slam_icp_set_schedule(4, 1024)
-        lib.slam_icp_set_schedule_gangs(24, 4)
+        lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
+        lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
+        lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
     assert single.iters.max() > 30
     for key, r in runs.items():
         assert np.array_equal(r.iters, single.iters), key
@@ -471,10 +491,12 @@ def test_gang_timeouts_are_repaired(k):
         assert lib.slam_icp_set_schedule(4, 1024) == 0
         assert lib.slam_icp_set_gang_wait(1) == 0
         lib.slam_icp_gang_timeouts()   # clear
-        for gangs, parts in ((64, 4), (16, 0)):
+        for gangs, parts, wide, bulk in ((64, 4, 0, 0), (16, 0, 0, 0), (0, 4, 16, 0), (8, 4, 0, 2), (0, 4, 0, 3)):
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
+            assert lib.slam_icp_set_schedule_wide(wide, 1) == 0
+            assert lib.slam_icp_set_bulk_gangs(4096 if bulk else 0, max(bulk, 2)) == 0
             r = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
-            assert lib.slam_icp_gang_timeouts() > 0, (gangs, parts)
+            assert lib.slam_icp_gang_timeouts() > 0, (gangs, parts, wide)
             assert np.array_equal(r.iters, single.iters), (gangs, parts)
             assert np.array_equal(r.tf, single.tf) and np.array_equal(r.err, single.err), (gangs, parts)
             for h0, h1 in zip(single.hist, r.hist):
@@ -482,7 +504,9 @@ def test_gang_timeouts_are_repaired(k):
     finally:
         lib.slam_icp_set_gang_wait(0)
         lib.slam_icp_set_schedule(4, 1024)
-        lib.slam_icp_set_schedule_gangs(24, 4)
+        lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
+        lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
+        lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
     assert lib.slam_icp_gang_timeouts() == 0
 
 

@@ -49,13 +49,21 @@ try:
         lib.slam_icp_set_schedule_gangs(0, 2)
         us, its, _ = timed(batch)
         line.append(f"head512x3:{us / its:.1f}")
-        for parts in (2, 4, 17, 0):
+        for parts in (4, 0):
             lib.slam_icp_set_schedule_gangs(1, parts)
             us, its2, r = timed(batch)
             assert its2 == its and np.array_equal(r.tf, ref.tf), (p, parts)
             line.append(f"{'team' if parts == 0 else 'gang' + str(parts)}:{us / its:.1f}")
+        lib.slam_icp_set_schedule_gangs(0, 4)
+        for share in (1, 2, 4):
+            lib.slam_icp_set_schedule_wide(1, share)
+            us, its2, r = timed(batch)
+            assert its2 == its and np.array_equal(r.tf, ref.tf), (p, "wide", share)
+            line.append(f"wide/{share}:{us / its:.1f}")
+        lib.slam_icp_set_schedule_wide(0, 1)
         print(f"pair {p} iters {its} us/iter (incl. 4 probe iterations on one workgroup) " + " ".join(line), flush=True)
 finally:
     lib.slam_icp_set_schedule(4, 1024)
     lib.slam_icp_set_schedule_heads(64)
     lib.slam_icp_set_schedule_gangs(24, 4)
+    lib.slam_icp_set_schedule_wide(0, 1)

@@ -1,0 +1,72 @@
+"""Per-pair timeline of one batched ICP launch (slam_icp_set_trace): for rank
+0's shard of the C3 stream, when each pair's workgroup started and ended in
+each scheduler phase, where (XCC / CU), and what bounds the makespan.  GPU only.
+
+    python tools/timeline.py [pairs ...]        (default 1250 2500)
+"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+
+
+def main():
+    import torch
+    torch.cuda.set_device(0)
+    from slamhip import _abi, se2, synthetic
+    from slamhip import icp as k
+    lib = _abi.lib()
+    sizes = [int(x) for x in sys.argv[1:]] or [1250, 2500]
+    n = max(sizes)
+    seq = synthetic.make_sequence(10001, seed=2025)
+    inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, n + 1)])
+    ss = k.ScanSet(seq.scans[:n + 1])
+    for P in sizes:
+        b = k.IcpBatch(ss, np.arange(1, P + 1), np.arange(0, P), inits[:P], epsilon=0.05, max_iters=100)
+        for _ in range(3):
+            b.launch()
+        torch.cuda.synchronize()
+        buf = torch.zeros(P * 8, dtype=torch.int64, device="cuda")
+        lib.slam_icp_set_trace(buf.data_ptr())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.launch()
+        e1.record()
+        torch.cuda.synchronize()
+        lib.slam_icp_set_trace(None)
+        ms = e0.elapsed_time(e1)
+        it = b.result().iters
+        t = buf.cpu().numpy().reshape(P, 2, 4)
+        st, en = t[:, :, 0].astype(np.float64), t[:, :, 1].astype(np.float64)
+        ran = st > 0
+        t0 = st[ran].min()
+        us = lambda x: (x - t0) / 100.0   # 100 MHz ticks -> us
+        end1 = np.where(ran[:, 0], us(en[:, 0]), np.nan)
+        st2 = np.where(ran[:, 1], us(st[:, 1]), np.nan)
+        end2 = np.where(ran[:, 1], us(en[:, 1]), np.nan)
+        fin = np.where(np.isnan(end2), end1, end2)
+        print(f"P {P}: event {ms * 1e3:.0f} us; phase 1 starts {np.nanmin(us(st[:, 0])):.0f}..{np.nanmax(us(st[:, 0])):.0f}"
+              f" ends {np.nanmin(end1):.0f}..{np.nanmax(end1):.0f}; phase 2 starts {np.nanmin(st2):.0f}..{np.nanmax(st2):.0f};"
+              f" last finish {np.nanmax(fin):.0f} us; pairs in phase 2: {int(ran[:, 1].sum())}", flush=True)
+        # finish-time quantiles and the last finishers
+        q = np.nanpercentile(fin, [50, 90, 99, 100])
+        print(f"   finish p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f} us", flush=True)
+        last = np.argsort(-np.nan_to_num(fin, nan=-1))[:12]
+        for j in last:
+            dur = (end2[j] - st2[j]) if not np.isnan(st2[j]) else np.nan
+            rem = it[j] - 4
+            print(f"   pair {j:5d} iters {it[j]:3d} p1 {us(st[j, 0]):6.0f}-{end1[j]:6.0f} p2 {st2[j]:6.0f}-{end2[j]:6.0f}"
+                  f" ({dur / max(rem, 1):5.1f} us/it) xcc {int(t[j, 1, 2]) >> 32} hw {int(t[j, 1, 2]) & 0xffffffff:#x}",
+                  flush=True)
+        # how many pairs are running over time (phase 2)
+        grid = np.arange(0, np.nanmax(fin) + 50, 50)
+        run = [int(np.sum((np.nan_to_num(st2, nan=1e18) <= g) & (np.nan_to_num(end2, nan=-1) > g))) for g in grid]
+        print("   phase-2 pairs running every 50 us: " + " ".join(str(r) for r in run), flush=True)
+        np.save(os.path.join(REPO, "gpurun_out", f"timeline_{P}.npy"), t)
+
+
+if __name__ == "__main__":
+    main()

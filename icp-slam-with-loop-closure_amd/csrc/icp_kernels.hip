@@ -89,6 +89,13 @@ struct IcpArgs {
     int32_t n_gangs;
     uint64_t* gang_slots;    // [n_gangs][2][gang][32] tagged granules, zeroed before the launch
     uint32_t gang_wait;      // longest wait for the partners of one exchange (s_memrealtime ticks)
+    // PRUNE kernels, scheduler phases: a paused pair's search state (per query
+    // i: last match and clearance word at qsave[b * qsave_stride + i]; the
+    // motion T_next - T and its slack at dtsave[b * 8 + ..]) so that its resumed
+    // iteration is as warm as an uninterrupted one (NULL: resume cold)
+    uint2* qsave;
+    float* dtsave;
+    int32_t qsave_stride;
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
 #ifndef SLAM_TAIL_SHARE
@@ -225,7 +232,7 @@ __device__ __forceinline__ void trace_mark(const IcpArgs& a, int b, int what) {
     if (a.trace) {
         unsigned long long* t = a.trace + (static_cast<int64_t>(b) * 2 + (a.resume ? 1 : 0)) * 4;
         t[what] = __builtin_amdgcn_s_memrealtime();
-        if (what == 0) t[2] = hw_where();
+        if (what == 0) t[2] = hw_where();   // slot 2: where; slot 3: staging done
     }
 }
 
@@ -901,23 +908,35 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     if (tid == 0 && part == 0) trace_mark(a, b, 0);
     const PairSetup ps = stage_pair<BLOCK, SCREEN, PRUNE>(a, n1, n2, p1, p2, resident, cand, candf, box8, red0, red1,
                                                           pconst);
+    if (tid == 0 && part == 0) trace_mark(a, b, 3);   // staging done (diagnostics)
     const double cmax = ps.cmax;
     const double pmaxd = ps.pmaxd;
     const float pmax = ps.pmax;
     const bool screen = ps.screen;
     const int nsub = ps.nsub;
     int bprev[QPT];   // !PRUNE screen: last match in registers
+    // a resumed pair with saved search state picks it up (PRUNE)
+    const bool warm = PRUNE && it0 > 0 && a.qsave != nullptr;
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
         bprev[k] = -1;
         if constexpr (PRUNE) {
-            qprev[k * BLOCK + tid] = -1;
-            qst[k * BLOCK + tid] = 0;   // clearance state (radius | window start), see st_pack
+            const int i = k * qstride + tid + gshift;
+            uint2 v = make_uint2(0xffffffffu, 0u);   // no match yet, clearance 0 (see st_pack)
+            if (warm && i < n1) v = a.qsave[static_cast<int64_t>(b) * a.qsave_stride + i];
+            qprev[k * BLOCK + tid] = static_cast<int>(v.x);
+            qst[k * BLOCK + tid] = v.y;
         }
     }
     int nscan_total = 0;
     // PRUNE: this iteration's motion T - T_prev in fp32 and its rounding slack
     float dT[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dsig = 0.0f;
+    if (warm) {
+        const float* ds = a.dtsave + static_cast<int64_t>(b) * 8;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) dT[q] = uniform_f(ds[q]);
+        dsig = uniform_f(ds[6]);
+    }
     const int n2_pad = (n2 + kChunk - 1) / kChunk * kChunk;
 
     // a resumed pair continues from its saved state: the transform and the
@@ -1324,6 +1343,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 // last error change orders the survivors for the next phase
                 flush_stamps();
                 if (counting && lane == 0) atomicAdd(a.evals, nev);
+                if constexpr (PRUNE) {
+                    if (a.qsave) {   // the search state, so the resumed iteration starts warm
+#pragma unroll
+                        for (int k = 0; k < QPT; ++k) {
+                            const int i = k * qstride + tid + gshift;
+                            if (i < n1)
+                                a.qsave[static_cast<int64_t>(b) * a.qsave_stride + i] =
+                                    make_uint2(static_cast<uint32_t>(qprev[k * BLOCK + tid]), qst[k * BLOCK + tid]);
+                        }
+                        if (tid == 0 && part == 0) {
+                            float* ds = a.dtsave + static_cast<int64_t>(b) * 8;
+#pragma unroll
+                            for (int q = 0; q < 6; ++q) ds[q] = dT[q];
+                            ds[6] = dsig;
+                        }
+                    }
+                }
                 if (tid == 0 && part == 0) {
                     store_se2(a.out_tf + 9 * static_cast<int64_t>(b), Tn);
                     a.out_err[b] = err;
@@ -2334,7 +2370,7 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
-static int g_sched_probe = 4;          // phase-1 iterations (0: single launch; 4-5 best on C3)
+static int g_sched_probe = 3;          // phase-1 iterations (0: single launch; 3 best on C3 since round 4)
 static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // Phase 2 starts the pairs the probe keyed slowest (the top g_sched_heads, at
 // most one per 16 pairs) on workgroups that request the whole LDS of a CU, so
@@ -2376,6 +2412,8 @@ static int g_wide_share = 1;
 // bulk as gangs of g_bulk_gang_parts workgroups (0 / 1 parts: off)
 static int g_bulk_gang_below = 0;
 static int g_bulk_gang_parts = 2;
+// carry the paused pairs' search state from phase 1 to phase 2 (warm resume)
+static int g_sched_warm = 0;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
@@ -2634,7 +2672,11 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const int nblk = (B + kSortBlock - 1) / kSortBlock;
     const size_t sched_bytes =
         (static_cast<size_t>(nblk) * kNB * sizeof(int32_t) + nb * (2 * sizeof(int32_t) + sizeof(float)) + 255) / 256 * 256;
-    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes;
+    // the paused pairs' search state (phase 1 -> 2): 8 B per query + 32 B per pair
+    const size_t qsave_bytes = g_sched_warm ? (nb * static_cast<size_t>(max_n1) * sizeof(uint2) + nb * 8 * sizeof(float) +
+                                               255) / 256 * 256
+                                           : 0;
+    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);   // hist_blk[nblk][kNB]
@@ -2648,6 +2690,12 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     IcpArgs a = args;
     a.phase_cap = probe;
     a.sched_key = key;
+    if (qsave_bytes) {
+        char* q0 = static_cast<char*>(ws) + sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes;
+        a.qsave = reinterpret_cast<uint2*>(q0);
+        a.dtsave = reinterpret_cast<float*>(q0 + nb * static_cast<size_t>(max_n1) * sizeof(uint2));
+        a.qsave_stride = max_n1;
+    }
     int rc;
     if (bg) {
         // a phase-1 gang that timed out writes nothing: its pair must then read
@@ -2807,6 +2855,12 @@ int slam_icp_set_bulk_gangs(int below_pairs, int parts) {
         return fail(SLAM_EINVAL, "bulk gangs: below %d parts %d", below_pairs, parts);
     g_bulk_gang_below = below_pairs;
     g_bulk_gang_parts = parts;
+    return ok();
+}
+// Diagnostics: carry the paused pairs' search state across the scheduler's
+// phase boundary (1, default) or resume them cold (0).  Results identical.
+int slam_icp_set_schedule_warm(int on) {
+    g_sched_warm = on ? 1 : 0;
     return ok();
 }
 int slam_icp_gang_timeouts(void) {

@@ -35,6 +35,7 @@ SIGNATURES = {
     "slam_icp_set_gang_wait": (c_int, [ctypes.c_uint32]),
     "slam_icp_set_schedule_wide": (c_int, [c_int, c_int]),
     "slam_icp_set_bulk_gangs": (c_int, [c_int, c_int]),
+    "slam_icp_set_schedule_warm": (c_int, [c_int]),
     "slam_icp_sched_sort": (c_int, [c_ptr, c_ptr, c_int, ctypes.c_float, c_ptr, c_ptr]),
     "slam_icp_set_eval_counter": (c_int, [c_ptr]),
     "slam_icp_set_trace": (c_int, [c_ptr]),

@@ -202,7 +202,7 @@ int slam_icp_set_screen(int mode);
  * every pair runs probe_iters iterations, then the unfinished ones resume in
  * order of their last error change (slowest-converging first), so the long
  * tail of iteration counts does not start late.  probe_iters = 0: one launch.
- * Defaults (4, 1024).  Results are identical either way. */
+ * Defaults (3, 1024).  Results are identical either way. */
 int slam_icp_set_schedule(int probe_iters, int min_pairs);
 /* Phase 2 of the scheduler starts the (at most) `heads` pairs the probe keyed
  * slowest (one per 16 pairs at most) first, on CU-exclusive 512-thread
@@ -235,6 +235,11 @@ int slam_icp_set_schedule_wide(int pairs, int share);
  * pairs cannot fill the GPU (strong-scaling shards).  Bit-identical results.
  * below_pairs = 0: off. */
 int slam_icp_set_bulk_gangs(int below_pairs, int parts);
+/* Diagnostics: the scheduler can save a paused pair's search state (last match
+ * and clearance per query, 8 B, and the pending motion bound) so its phase-2
+ * iteration starts warm (1; a transient workspace of 8 B per query — measured
+ * no faster on C3, round 4); 0 (default) resumes cold.  Results are identical. */
+int slam_icp_set_schedule_warm(int on);
 /* Gang parts that waited longer than the gang wait (default 0.2 s) for a
  * partner since the last call (read-and-clear; synchronises the device).  Such
  * a part stops at once without writing; after phase 2 the scheduler re-runs

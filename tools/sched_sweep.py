@@ -1,7 +1,7 @@
 """Scheduler settings vs batch size, in one process: rank 0's shard of the C3
 stream (first P pairs) for P in 1250 / 2500 / 5000 / 10000, timed with HIP
 events (median of 7 launches) under each setting
-"heads,gangs,parts,wide,share,bulk_below,bulk_parts,probe".  GPU only.
+"heads,gangs,parts,wide,share,bulk_below,bulk_parts,probe[,warm]".  GPU only.
 
     python tools/sched_sweep.py [setting ...]
 """
@@ -44,7 +44,9 @@ def main():
     ref = {}
     try:
         for st in settings:
-            h, g, gp, w, ws, bb, bp, pr = (int(x) for x in st.split(","))
+            v = [int(x) for x in st.split(",")]
+            h, g, gp, w, ws, bb, bp, pr = v[:8]
+            assert lib.slam_icp_set_schedule_warm(v[8] if len(v) > 8 else 1) == 0
             assert lib.slam_icp_set_schedule_heads(h) == 0
             assert lib.slam_icp_set_schedule_gangs(g, gp) == 0
             assert lib.slam_icp_set_schedule_wide(w, ws) == 0
@@ -74,7 +76,8 @@ def main():
         lib.slam_icp_set_schedule_gangs(24, 4)
         lib.slam_icp_set_schedule_wide(0, 1)
         lib.slam_icp_set_bulk_gangs(0, 2)
-        lib.slam_icp_set_schedule(4, 1024)
+        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule_warm(1)
 
 
 if __name__ == "__main__":

@@ -51,6 +51,12 @@ def main():
         print(f"P {P}: event {ms * 1e3:.0f} us; phase 1 starts {np.nanmin(us(st[:, 0])):.0f}..{np.nanmax(us(st[:, 0])):.0f}"
               f" ends {np.nanmin(end1):.0f}..{np.nanmax(end1):.0f}; phase 2 starts {np.nanmin(st2):.0f}..{np.nanmax(st2):.0f};"
               f" last finish {np.nanmax(fin):.0f} us; pairs in phase 2: {int(ran[:, 1].sum())}", flush=True)
+        # staging latency (start -> pc2 staged, constants ready) and per-iteration latency
+        for ph in (0, 1):
+            ok = ran[:, ph] & (t[:, ph, 3] > 0)
+            stg = (t[ok, ph, 3].astype(np.float64) - st[ok, ph]) / 100.0
+            print(f"   phase {ph + 1} staging latency us: p50 {np.median(stg):.1f} p90 {np.percentile(stg, 90):.1f}",
+                  flush=True)
         # finish-time quantiles and the last finishers
         q = np.nanpercentile(fin, [50, 90, 99, 100])
         print(f"   finish p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f} us", flush=True)

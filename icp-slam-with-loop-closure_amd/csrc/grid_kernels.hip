@@ -46,9 +46,11 @@ __global__ __launch_bounds__(kGridBlock) void grid_points_kernel(const double2* 
     double bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
     for (int64_t j = scan_off[s] + threadIdx.x; j < scan_off[s + 1]; j += kGridBlock) {
         const double2 p = pts[j];
-        // [c -s x; s c y] [p; 1] with the k = 0, 1, 2 FMA chain
-        const double gx = fma(px, 1.0, fma(-sn, p.y, c * p.x));
-        const double gy = fma(py, 1.0, fma(c, p.y, sn * p.x));
+        // [c -s x; s c y] [p; 1] exactly as NumPy's 3x3 @ 3x1 product rounds it on
+        // the build host (OpenBLAS: fma(a0, x0, a1 x1) + a2 x2, found by brute force
+        // over every association and fusion; tests/golden/grid_ref.npz pins it)
+        const double gx = fma(c, p.x, -sn * p.y) + px;
+        const double gy = fma(sn, p.x, c * p.y) + py;
         gpts[j] = make_double2(gx, gy);
         bx0 = fmin(bx0, gx);
         bx1 = fmax(bx1, gx);

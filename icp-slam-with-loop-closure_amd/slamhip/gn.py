@@ -31,14 +31,16 @@ LOOP_INFO = 5.0
 class GnPlan:
     """Symbolic analysis of one graph structure."""
 
-    def __init__(self, N, ea, eb, fixed=0):
+    def __init__(self, N, ea, eb, fixed=0, order=None):
         ea = np.asarray(ea, dtype=np.int64)
         eb = np.asarray(eb, dtype=np.int64)
         self.N = N
         self.fixed = fixed
-        adj = sp.coo_matrix((np.ones(2 * len(ea) + N), (np.r_[ea, eb, np.arange(N)], np.r_[eb, ea, np.arange(N)])),
-                            shape=(N, N)).tocsr()
-        order = reverse_cuthill_mckee(adj, symmetric_mode=True)
+        if order is None:
+            adj = sp.coo_matrix((np.ones(2 * len(ea) + N), (np.r_[ea, eb, np.arange(N)], np.r_[eb, ea, np.arange(N)])),
+                                shape=(N, N)).tocsr()
+            order = reverse_cuthill_mckee(adj, symmetric_mode=True)
+        order = np.asarray(order, dtype=np.int64)
         order = order[order != fixed]
         node_col = np.full(N, -1, dtype=np.int32)
         node_col[order] = 3 * np.arange(len(order), dtype=np.int32)

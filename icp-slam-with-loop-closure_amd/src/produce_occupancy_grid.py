@@ -18,9 +18,9 @@ Same functions and return types as the reference
   reference uses cv2.imwrite, and OpenCV is not part of this build).
 
 Deviation (checked): kHitOdds and kMissOdds must be integers in [1, 127].
-Global points use the dgemm FMA order; the reference's per-point 3x3 @ 3x1
-product can round the last bit differently, which changes a cell index only
-for a point lying exactly on a cell boundary.
+Global points are rounded as the reference's per-point 3x3 @ 3x1 NumPy product
+rounds them on the build host (fma(a0, x0, a1 x1) + a2 x2), so grids and origins
+match the reference's own functions bit for bit (tests/golden/grid_ref.npz).
 """
 import struct
 import zlib

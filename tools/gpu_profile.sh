@@ -5,12 +5,12 @@
 #   separate passes; FETCH_SIZE under-reports wide coalesced reads by 2x), then
 #   the instruction mix (VALU / SALU / LDS instructions, waves).
 set -e
-TAG=${1:-r03}
+TAG=${1:-r04}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o icp -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pgo > $OUT/bench_traced.json 2> $OUT/bench_traced.err
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pgo > $OUT/bench_traced.json 2> $OUT/bench_traced.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o f -- \
     python3 tools/prof_icp.py 10000 1 > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o w -- \

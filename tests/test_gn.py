@@ -64,6 +64,27 @@ def test_plan_covers_every_edge():
     assert p.W == max(2, np.abs(cols[ea][both] - cols[eb][both]).max() + 2)
 
 
+def test_place_major_order_on_c4():
+    """C4's lap structure: the place-major order (places = components of the
+    loop-closure edges, RCM over the place graph) gives a 62-scalar band
+    (BCR blocks of 64 rows) where RCM over the poses gives 77 (80-row blocks);
+    band_order keeps RCM where places do not narrow the band."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    from slamhip import gn, synthetic
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
+    N = len(guess)
+    p = gn.GnPlan(N, ea, eb)
+    assert p.ordering == "place-major" and p.W == 62
+    order = gn.place_order(N, np.asarray(ea, np.int64), np.asarray(eb, np.int64))
+    assert sorted(order.tolist()) == list(range(N))
+    adj = sp.coo_matrix((np.ones(2 * len(ea)), (np.r_[ea, eb], np.r_[eb, ea])), shape=(N, N)).tocsr()
+    assert gn.GnPlan(N, ea, eb, order=reverse_cuthill_mckee(adj, symmetric_mode=True)).W == 77
+    # sparse loops (incomplete places): RCM stays
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=25, num_loops=3, n_loops=200)
+    assert gn.GnPlan(len(guess), ea, eb).ordering == "rcm"
+
+
 def test_oracle_converges_on_c4():
     from slamhip import synthetic
     guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=25, num_loops=4, n_loops=300)

@@ -47,9 +47,13 @@ __device__ inline void bcr_rc(int e, int Wb, float inv, int& r, int& c) {
 
 // Band (row r holds (r, r-d), d = 0..W) -> D_i (full symmetric), E_i, b_i;
 // rows past nv are padded with the identity.
+// Bordered solves (mc > 1): the right-hand side of block row i is Wb x mc,
+// column 0 the rhs and column 1 + k the border column k of H (BR row k: H's
+// row nv + k, row stride nvt), zero padded.
 __global__ void bcr_load_kernel(const double* __restrict__ Hb, const double* __restrict__ rhs, int32_t nv,
                                 int32_t W, int32_t Wb, int32_t nb, double* __restrict__ D, double* __restrict__ E,
-                                double* __restrict__ bz) {
+                                double* __restrict__ bz, int32_t mc, const double* __restrict__ BR, int32_t nbd,
+                                int32_t nvt) {
     const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (idx >= nb * bcr_blk(Wb)) return;
     const int i = static_cast<int>(idx / bcr_blk(Wb));
@@ -68,7 +72,15 @@ __global__ void bcr_load_kernel(const double* __restrict__ Hb, const double* __r
         const int R2 = R + Wb, d2 = R2 - Cc;
         E[idx] = (R2 < nv && d2 <= W) ? Hb[R2 * ld + d2] : 0.0;
     }
-    if (c == 0) bz[static_cast<int64_t>(i) * Wb + r] = R < nv ? rhs[R] : 0.0;
+    if (mc == 1) {
+        if (c == 0) bz[static_cast<int64_t>(i) * Wb + r] = R < nv ? rhs[R] : 0.0;
+    } else {
+        for (int cc = c; cc < mc; cc += Wb) {   // mc may exceed Wb
+            double v = 0.0;
+            if (R < nv) v = cc == 0 ? rhs[R] : cc <= nbd ? BR[static_cast<int64_t>(cc - 1) * nvt + R] : 0.0;
+            bz[static_cast<int64_t>(R) * mc + cc] = v;
+        }
+    }
 }
 
 // The augmented elimination of a register-tiled [D | R] (16 x 16 threads,
@@ -972,16 +984,19 @@ int bcr_block_rows(int32_t nv, int32_t W) {
     return Wb;
 }
 
-int64_t bcr_work_size(int32_t nv, int32_t W) {
+int64_t bcr_work_size(int32_t nv, int32_t W, int32_t mc) {
     const int Wb = ((max(W, 1) + 15) / 16) * 16;
     const int64_t nb = (nv + Wb - 1) / Wb;
-    return max(5 * nb * bcr_blk(Wb) + 2 * nb * Wb, bcr_gj_work_size(nv, Wb));
+    return max(5 * nb * bcr_blk(Wb) + 2 * nb * Wb, bcr_gj_work_size(nv, Wb, mc));
 }
 
 // Solve H dx = rhs (H in band storage, work of bcr_work_size doubles); *dx_out
 // points at the solution inside `work` (first nv entries).
+// Bordered (mc > 1, explicit-inverse path only): the mc right-hand sides of
+// bcr_load_kernel; *dx_out is then the nv x mc solution block (row stride mc).
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
-              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps) {
+              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
+              const double* BR, int32_t nbd, int32_t nvt) {
     const int nb = (nv + Wb - 1) / Wb;
     const int64_t B2 = bcr_blk(Wb);
     // default: the explicit-inverse levels (gn_bcr_gj.hip); the Cholesky paths
@@ -991,14 +1006,14 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         const char* l = getenv("SLAMHIP_BCR_LEGACY");
         return (e && e[0] == '1') || (l && l[0] == '1');
     }();
-    if (!chol) {
-        const BcrGjBufs g = bcr_gj_bufs(work, nv, Wb);
+    if (!chol || mc > 1) {
+        const BcrGjBufs g = bcr_gj_bufs(work, nv, Wb, mc);
         const int64_t tot = nb * B2;
         hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs,
-                           nv, W, Wb, nb, g.D, g.E0, g.bz);
-        int rc = bcr_gj_levels(g, nv, Wb, status, st);   // levels + block 0
+                           nv, W, Wb, nb, g.D, g.E0, g.bz, mc, BR, nbd, nvt);
+        int rc = bcr_gj_levels(g, nv, Wb, mc, status, st);   // levels + block 0
         if (rc != 0) return rc;
-        rc = bcr_gj_back(g, nv, Wb, st);
+        rc = bcr_gj_back(g, nv, Wb, mc, st);
         *dx_out = g.x;
         return rc;
     }
@@ -1012,7 +1027,7 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
     *dx_out = dx;
     const int64_t tot = nb * B2;
     hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs, nv,
-                       W, Wb, nb, D, E, bz);
+                       W, Wb, nb, D, E, bz, 1, nullptr, 0, nv);
     const size_t lds_even = sizeof(double) * (2 * static_cast<size_t>(Wb) * (Wb + 1) + 2 * static_cast<size_t>(Wb));
     const size_t lds_back = sizeof(double) * (static_cast<size_t>(Wb) * (Wb + 1) + 4 * static_cast<size_t>(Wb));
     using EvenFn = void (*)(double*, double*, const double*, const double*, double*, int32_t, int32_t, int32_t);

@@ -12,11 +12,11 @@ namespace slamhip {
 // workspace carve-up of the explicit-inverse path (nb = ceil(nv / Wb) blocks)
 struct BcrGjBufs {
     double *D, *E0, *E1, *Xs, *Ys, *SP, *SN;   // nb x Wb x Wb each
-    double *bz, *SPb, *SNb, *x;                // nb x Wb each
+    double *bz, *SPb, *SNb, *x;                // nb x Wb x mc each (mc right-hand-side columns)
 };
-BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb);
-int64_t bcr_gj_work_size(int32_t nv, int32_t Wb);
-int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, hipStream_t st);
-int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, hipStream_t st);
+BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc);
+int64_t bcr_gj_work_size(int32_t nv, int32_t Wb, int32_t mc);
+int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_t* status, hipStream_t st);
+int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st);
 
 }  // namespace slamhip

@@ -66,6 +66,8 @@ struct Lds {
     static constexpr int LDC = 17;       // one column tile: [WB][LDC]
     static constexpr size_t doubles = static_cast<size_t>(WB) * LDA + static_cast<size_t>(WB) * LDC + 2 * WB;
     static constexpr size_t bytes = doubles * sizeof(double);
+    // bordered solves (several right-hand-side columns): + one RHS column tile
+    static constexpr size_t bytes_multi = bytes + static_cast<size_t>(WB) * LDC * sizeof(double);
 };
 
 // D_i (WB x WB, global, row-major) -> A (LDS): every load in flight at once.
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
                                                       double* __restrict__ Ys, double* __restrict__ SP,
                                                       double* __restrict__ SN, double* __restrict__ bz,
                                                       double* __restrict__ SPb, double* __restrict__ SNb, int32_t nb,
-                                                      int32_t s, int32_t cpw, int32_t n_odd,
+                                                      int32_t s, int32_t cpw, int32_t n_odd, int32_t mc,
                                                       int32_t* __restrict__ status) {
     using L = Lds<T>;
     constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, K4 = WB / 4;
@@ -269,7 +271,12 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
     double* A = lds;
     double* C = A + WB * LDA;
     double* vz = C + WB * LDC;   // [2][WB]: b_i, z_i
+    double* Rt = vz + 2 * WB;    // mc > 1: the workgroup's RHS column tile [WB][LDC]
     const int ng = (T + cpw - 1) / cpw;
+    // mc > 1 (bordered solve): the right-hand side is a
+    // WB x mc block per block row (row stride mc) in mc / 16 column tiles, one
+    // workgroup per tile (q = 2 ng + tile) instead of the mat-vec workgroup
+    const int mct = mc > 1 ? mc / 16 : 0;
     const int q = blockIdx.y;
     const int sp = s / 2;   // the previous level (0: none)
     const int tid = threadIdx.x;
@@ -287,25 +294,27 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
             if (h2) v -= SP[(j + sp) * B2 + e];
             Dj[e] = v;
         }
-        if (q == 0 && tid < WB) {
-            double v = bz[static_cast<int64_t>(j) * WB + tid];
-            if (h1) v -= SNb[static_cast<int64_t>(j - sp) * WB + tid];
-            if (h2) v -= SPb[static_cast<int64_t>(j + sp) * WB + tid];
-            bz[static_cast<int64_t>(j) * WB + tid] = v;
+        const int64_t RB = static_cast<int64_t>(WB) * mc;   // RHS doubles per block
+        for (int64_t e = q * kThreads + tid; e < RB; e += kCombineSplit * kThreads) {
+            double v = bz[j * RB + e];
+            if (h1) v -= SNb[(j - sp) * RB + e];
+            if (h2) v -= SPb[(j + sp) * RB + e];
+            bz[j * RB + e] = v;
         }
         return;
     }
-    if (q > 2 * ng) return;   // grid.y padded for the combine workgroups
+    if (q > 2 * ng + (mct > 0 ? mct - 1 : 0)) return;   // grid.y padded for the combine workgroups
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
     const bool hn = n < nb;
-    // side 0: X / Sp / E', 2: Y / Sn, 3: z
-    const int side = q == 2 * ng ? 3 : (q < ng ? 0 : 2);
+    // side 0: X / Sp / E', 2: Y / Sn, 3: z (mat-vecs), 4: RHS column tile q - 2 ng
+    const int side = q >= 2 * ng ? (mct > 0 ? 4 : 3) : (q < ng ? 0 : 2);
     const bool zwg = side == 3;
+    const bool rwg = side == 4;
     const bool xside = side == 0;
     if (side == 2 && !hn) return;   // the last block has no right neighbour
     const int g0 = (q % ng) * cpw;
-    const int tj0 = zwg ? 0 : g0, tj1 = zwg ? 0 : min(T, g0 + cpw);
+    const int tj0 = zwg ? 0 : rwg ? q - 2 * ng : g0, tj1 = zwg ? 0 : rwg ? q - 2 * ng + 1 : min(T, g0 + cpw);
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 15, lk = lane >> 4;
@@ -347,6 +356,19 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
             A[(e / WB) * LDA + e % WB] = g[qq];
         }
     }
+    if (rwg) {
+        // RHS tile with the previous level's updates folded in (as D_i)
+        const int64_t RB = static_cast<int64_t>(WB) * mc;
+        for (int e = tid; e < WB * 16; e += kThreads) {
+            const int r = e >> 4, c = 16 * tj0 + (e & 15);
+            double v = bz[i * RB + r * mc + c];
+            if (sp > 0) {
+                v -= SNb[(i - sp) * RB + r * mc + c];
+                if (i + sp < nb) v -= SPb[(i + sp) * RB + r * mc + c];
+            }
+            Rt[r * LDC + (e & 15)] = v;
+        }
+    }
     if (zwg && tid < WB) {
         double v = bz[static_cast<int64_t>(i) * WB + tid];
         if (sp > 0) {
@@ -364,13 +386,18 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
         // first product: column tile tj of X_i = G E_p or Y_i = G E_i^T: the
         // tile of E (the B operand, shared by every output tile) is loaded once,
         // all K4 fragments in flight; a wave's output tiles run interleaved
-        double* Out1 = (xside ? Xs : Ys) + i * B2;
+        // RHS tile: z_i's columns 16 tj.. (bz, row stride mc), then E_p^T z (SPb)
+        // and E_i z (SNb) as the X side's Sp and E' (sign +)
+        const int64_t RB = static_cast<int64_t>(WB) * mc;
+        double* Out1 = rwg ? bz + i * RB + 16 * tj : (xside ? Xs : Ys) + i * B2 + 16 * tj;
+        const int ld1 = rwg ? mc : WB;
         {
             constexpr int N1 = (T + 3) / 4;
             double bf[K4];
 #pragma unroll
             for (int k4 = 0; k4 < K4; ++k4)
-                bf[k4] = xside ? Ep[(4 * k4 + lk) * WB + 16 * tj + lr] : Ei[(16 * tj + lr) * WB + 4 * k4 + lk];
+                bf[k4] = rwg ? Rt[(4 * k4 + lk) * LDC + lr]
+                             : xside ? Ep[(4 * k4 + lk) * WB + 16 * tj + lr] : Ei[(16 * tj + lr) * WB + 4 * k4 + lk];
             f64x4 acc[N1];
 #pragma unroll
             for (int u = 0; u < N1; ++u) acc[u] = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -388,7 +415,7 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
                         const int row = 16 * ti + lk + 4 * g;
-                        Out1[row * WB + 16 * tj + lr] = acc[u][g];
+                        Out1[row * ld1 + lr] = acc[u][g];
                         C[row * LDC + lr] = acc[u][g];
                     }
                 }
@@ -401,7 +428,7 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
         // in flight at once
         {
             constexpr int N2 = (2 * T + 3) / 4;
-            const int ntask = (xside && hn) ? 2 * T : T;
+            const int ntask = ((xside || rwg) && hn) ? 2 * T : T;
             double bf[K4];
 #pragma unroll
             for (int k4 = 0; k4 < K4; ++k4) bf[k4] = C[(4 * k4 + lk) * LDC + lr];
@@ -410,18 +437,20 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
                 const int t = wave + 4 * u;
                 if (t < ntask) {   // wave-uniform
                     const int ti = t % T;
-                    const bool e = t >= T;   // X side: the new coupling
+                    const bool e = t >= T;   // X side: the new coupling; RHS tile: E_i z
                     double af[K4];
 #pragma unroll
                     for (int k4 = 0; k4 < K4; ++k4)
-                        af[k4] = (xside && !e) ? Ep[(4 * k4 + lk) * WB + 16 * ti + lr] : Ei[(16 * ti + lr) * WB + 4 * k4 + lk];
+                        af[k4] = ((xside || rwg) && !e) ? Ep[(4 * k4 + lk) * WB + 16 * ti + lr]
+                                                        : Ei[(16 * ti + lr) * WB + 4 * k4 + lk];
                     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                     for (int k4 = 0; k4 < K4; ++k4) acc = mma(af[k4], bf[k4], acc);
-                    double* Out2 = e ? En + p * B2 : xside ? SP + i * B2 : SN + i * B2;
-                    const double sg = e ? -1.0 : 1.0;
+                    double* Out2 = rwg ? (e ? SNb : SPb) + i * RB + 16 * tj
+                                       : (e ? En + p * B2 : xside ? SP + i * B2 : SN + i * B2) + 16 * tj;
+                    const double sg = (e && !rwg) ? -1.0 : 1.0;
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) Out2[(16 * ti + lk + 4 * g) * WB + 16 * tj + lr] = sg * acc[g];
+                    for (int g = 0; g < 4; ++g) Out2[(16 * ti + lk + 4 * g) * ld1 + lr] = sg * acc[g];
                 }
             }
         }
@@ -473,7 +502,8 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
 template <int T>
 __global__ __launch_bounds__(kThreads) void top_kernel(const double* __restrict__ D, const double* __restrict__ SP,
                                                       const double* __restrict__ bz, const double* __restrict__ SPb,
-                                                      double* __restrict__ x, int32_t sl, int32_t* __restrict__ status) {
+                                                      double* __restrict__ x, int32_t sl, int32_t mc,
+                                                      int32_t* __restrict__ status) {
     using L = Lds<T>;
     constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, PER = T * T, KQ = WB / 4;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -495,6 +525,27 @@ __global__ __launch_bounds__(kThreads) void top_kernel(const double* __restrict_
             const int e = tid + kThreads * qq;
             A[(e / WB) * LDA + e % WB] = sl > 0 ? g[qq] - a1[qq] : g[qq];
         }
+    }
+    if (mc > 1) {
+        // bordered solve: X_0 = G R_0 for the WB x mc right-hand side (R in LDS
+        // behind vz, row stride mc + 1); each thread sums whole dot products
+        double* R = vz + 2 * WB;
+        const int64_t RB = static_cast<int64_t>(WB) * mc;
+        for (int e = tid; e < WB * mc; e += kThreads) {
+            const int r = e / mc, c = e % mc;
+            R[r * (mc + 1) + c] = sl > 0 ? bz[e] - SPb[sl * RB + e] : bz[e];
+        }
+        __syncthreads();
+        const bool bad = gj_invert<T>(A, C);
+        if (bad && tid == 0) *status = 1;
+        for (int e = tid; e < WB * mc; e += kThreads) {
+            const int r = e / mc, c = e % mc;
+            double acc = 0.0;
+#pragma unroll 8
+            for (int k = 0; k < WB; ++k) acc = fma(A[r * LDA + k], R[k * (mc + 1) + c], acc);
+            x[e] = acc;
+        }
+        return;
     }
     if (tid < WB) vz[tid] = sl > 0 ? bz[tid] - SPb[static_cast<int64_t>(sl) * WB + tid] : bz[tid];
     __syncthreads();
@@ -584,13 +635,58 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
     }
 }
 
+// Bordered solves: x_i = z_i - X_i x_p - Y_i x_n for WB x mc blocks (row
+// stride mc, mc a multiple of 16); x_p and x_n staged in LDS.  Thread t takes
+// row r and 4 consecutive columns per pass (fixed k order: deterministic).
+template <int T>
+__global__ __launch_bounds__(kThreads) void back_multi_kernel(const double* __restrict__ Xs,
+                                                             const double* __restrict__ Ys,
+                                                             const double* __restrict__ bz, double* __restrict__ x,
+                                                             int32_t nb, int32_t s, int32_t mc) {
+    constexpr int WB = 16 * T;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xp = lds;             // [WB][mc]
+    double* xn = xp + WB * mc;    // [WB][mc]
+    const int tid = threadIdx.x;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const bool hn = n < nb;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
+    for (int e = tid; e < WB * mc; e += kThreads) {
+        xp[e] = x[p * RB + e];
+        xn[e] = hn ? x[n * RB + e] : 0.0;
+    }
+    __syncthreads();
+    const double* X = Xs + i * B2;
+    const double* Y = Ys + i * B2;
+    const int cq = mc / 4;   // column quads per row
+    for (int e = tid; e < WB * cq; e += kThreads) {
+        const int r = e / cq, c0 = 4 * (e % cq);
+        double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int k = 0; k < WB; ++k) {
+            const double xv = X[r * WB + k], yv = hn ? Y[r * WB + k] : 0.0;
+            const double4 u = *reinterpret_cast<const double4*>(xp + k * mc + c0);
+            const double4 v = *reinterpret_cast<const double4*>(xn + k * mc + c0);
+            a[0] = fma(xv, u.x, fma(yv, v.x, a[0]));
+            a[1] = fma(xv, u.y, fma(yv, v.y, a[1]));
+            a[2] = fma(xv, u.z, fma(yv, v.z, a[2]));
+            a[3] = fma(xv, u.w, fma(yv, v.w, a[3]));
+        }
+        const int64_t o = i * RB + r * mc + c0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[o + q] = bz[o + q] - a[q];
+    }
+}
+
 }  // namespace bcrgj
 
 constexpr int kBcrGjSlots = 2 * 256;   // odd-kernel workgroups resident at once (2 per CU)
 
-BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb) {
+BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc) {
     const int64_t nb = (nv + Wb - 1) / Wb;
     const int64_t B2 = static_cast<int64_t>(Wb) * Wb;
+    const int64_t RB = static_cast<int64_t>(Wb) * mc;
     BcrGjBufs b;
     b.D = work;
     b.E0 = b.D + nb * B2;
@@ -600,32 +696,37 @@ BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb) {
     b.SP = b.Ys + nb * B2;
     b.SN = b.SP + nb * B2;
     b.bz = b.SN + nb * B2;
-    b.SPb = b.bz + nb * Wb;
-    b.SNb = b.SPb + nb * Wb;
-    b.x = b.SNb + nb * Wb;
+    b.SPb = b.bz + nb * RB;
+    b.SNb = b.SPb + nb * RB;
+    b.x = b.SNb + nb * RB;
     return b;
 }
 
-int64_t bcr_gj_work_size(int32_t nv, int32_t Wb) {
+int64_t bcr_gj_work_size(int32_t nv, int32_t Wb, int32_t mc) {
     const int64_t nb = (nv + Wb - 1) / Wb;
-    return 7 * nb * Wb * Wb + 4 * nb * Wb;
+    return 7 * nb * Wb * Wb + 4 * nb * Wb * static_cast<int64_t>(mc);
 }
 
 // The levels of the explicit-inverse reduction, after bcr_load_kernel filled
 // D, E0 and bz, and the block-0 solve (x_0 in b.x).
-int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, hipStream_t st) {
+int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_t* status, hipStream_t st) {
     const int nb = (nv + Wb - 1) / Wb;
+    const int mct = mc > 1 ? mc / 16 : 0;   // RHS column tiles (bordered solves)
     using OddFn = void (*)(double*, const double*, double*, double*, double*, double*, double*, double*,
-                           double*, double*, int32_t, int32_t, int32_t, int32_t, int32_t*);
+                           double*, double*, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t*);
     static const OddFn odds[6] = {bcrgj::odd_kernel<1>, bcrgj::odd_kernel<2>, bcrgj::odd_kernel<3>,
                                   bcrgj::odd_kernel<4>, bcrgj::odd_kernel<5>, bcrgj::odd_kernel<6>};
-    static const size_t lds[6] = {bcrgj::Lds<1>::bytes, bcrgj::Lds<2>::bytes, bcrgj::Lds<3>::bytes,
-                                  bcrgj::Lds<4>::bytes, bcrgj::Lds<5>::bytes, bcrgj::Lds<6>::bytes};
+    static const size_t lds1[6] = {bcrgj::Lds<1>::bytes, bcrgj::Lds<2>::bytes, bcrgj::Lds<3>::bytes,
+                                   bcrgj::Lds<4>::bytes, bcrgj::Lds<5>::bytes, bcrgj::Lds<6>::bytes};
+    static const size_t ldsm[6] = {bcrgj::Lds<1>::bytes_multi, bcrgj::Lds<2>::bytes_multi,
+                                   bcrgj::Lds<3>::bytes_multi, bcrgj::Lds<4>::bytes_multi,
+                                   bcrgj::Lds<5>::bytes_multi, bcrgj::Lds<6>::bytes_multi};
+    const size_t* lds = mct > 0 ? ldsm : lds1;
     static bool attrs = false;
     if (!attrs) {   // not a stream operation: the launch sequence stays graph-capturable
         for (int t = 0; t < 6; ++t)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(odds[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      static_cast<int>(lds[t]));
+                                      static_cast<int>(ldsm[t]));
         attrs = true;
     }
     const int T = Wb / 16;
@@ -642,7 +743,7 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, h
         int cpw = T;
         double best = 1e30;
         for (int c = 1; c <= T; ++c) {
-            const int wgs = n_odd * (2 * ((T + c - 1) / c) + 1);
+            const int wgs = n_odd * (2 * ((T + c - 1) / c) + max(mct, 1));
             const int rounds = (wgs + kBcrGjSlots - 1) / kBcrGjSlots;
             const double est = rounds * (42.0 + c * 17.0);
             if (est < best) {
@@ -653,38 +754,49 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t* status, h
         const int ng = (T + cpw - 1) / cpw;
         // + the combine workgroups of the blocks that stay even (j = 0, 2s, ...)
         const int n_comb = s > 1 ? n_even : 0;
-        hipLaunchKernelGGL(odds[T - 1], dim3(n_odd + n_comb, max(2 * ng + 1, bcrgj::kCombineSplit)),
+        hipLaunchKernelGGL(odds[T - 1], dim3(n_odd + n_comb, max(2 * ng + max(mct, 1), bcrgj::kCombineSplit)),
                            dim3(bcrgj::kThreads), lds[T - 1], st, b.D, Ec, En, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb,
-                           b.SNb, nb, s, cpw, n_odd, status);
+                           b.SNb, nb, s, cpw, n_odd, mc, status);
         last = s;
     }
     // block 0 (always even): the last level's Sp, then x_0
-    using TopFn = void (*)(const double*, const double*, const double*, const double*, double*, int32_t, int32_t*);
+    using TopFn = void (*)(const double*, const double*, const double*, const double*, double*, int32_t, int32_t,
+                           int32_t*);
     static const TopFn tops[6] = {bcrgj::top_kernel<1>, bcrgj::top_kernel<2>, bcrgj::top_kernel<3>,
                                   bcrgj::top_kernel<4>, bcrgj::top_kernel<5>, bcrgj::top_kernel<6>};
     static bool attrs_t = false;
     if (!attrs_t) {
         for (int t = 0; t < 6; ++t)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tops[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      static_cast<int>(lds[t]));
+                                      static_cast<int>(lds1[t] + sizeof(double) * 96 * 65));
         attrs_t = true;
     }
-    hipLaunchKernelGGL(tops[T - 1], dim3(1), dim3(bcrgj::kThreads), lds[T - 1], st, b.D, b.SP, b.bz, b.SPb, b.x,
-                       nb > 1 ? last : 0, status);
+    const size_t lds_top = lds1[T - 1] + (mct > 0 ? sizeof(double) * Wb * (mc + 1) : 0);
+    hipLaunchKernelGGL(tops[T - 1], dim3(1), dim3(bcrgj::kThreads), lds_top, st, b.D, b.SP, b.bz, b.SPb, b.x,
+                       nb > 1 ? last : 0, mc, status);
     return check_launch("gn bcr (explicit inverse) kernels");
 }
 
 // Back-substitution, level by level in reverse, after the top kernel wrote x_0.
-int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, hipStream_t st) {
+int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st) {
     const int nb = (nv + Wb - 1) / Wb;
     using BackFn = void (*)(const double*, const double*, const double*, double*, int32_t, int32_t);
     static const BackFn backs[6] = {bcrgj::back_kernel<1>, bcrgj::back_kernel<2>, bcrgj::back_kernel<3>,
                                     bcrgj::back_kernel<4>, bcrgj::back_kernel<5>, bcrgj::back_kernel<6>};
+    using BackMFn = void (*)(const double*, const double*, const double*, double*, int32_t, int32_t, int32_t);
+    static const BackMFn backms[6] = {bcrgj::back_multi_kernel<1>, bcrgj::back_multi_kernel<2>,
+                                      bcrgj::back_multi_kernel<3>, bcrgj::back_multi_kernel<4>,
+                                      bcrgj::back_multi_kernel<5>, bcrgj::back_multi_kernel<6>};
     int s = 1;
     while (s < nb) s *= 2;
     for (s /= 2; s >= 1; s /= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
-        hipLaunchKernelGGL(backs[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bz, b.x, nb, s);
+        if (mc > 1)
+            hipLaunchKernelGGL(backms[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads),
+                               2 * sizeof(double) * Wb * mc, st, b.Xs, b.Ys, b.bz, b.x, nb, s, mc);
+        else
+            hipLaunchKernelGGL(backs[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bz, b.x,
+                               nb, s);
     }
     return check_launch("gn bcr (explicit inverse) back-substitution");
 }

@@ -107,9 +107,12 @@ __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int3
 // use A'WA / A'We; side 1: target, B'WB / B'We).  Pair slots (r0 > c0) list
 // items 2e + o: o = 0 when e's source is the ROW node (block = A'WB), o = 1
 // when e's target is the row node (block = (A'WB)^T).
+// Bordered plans: rows R >= nv_band (the border's scalars, ordered last) go to
+// the dense border rows BR[(R - nv_band) * nvt + C] (C <= R) instead of the band.
 __global__ void gn_assemble_kernel(const double* __restrict__ contrib, const int32_t* __restrict__ slot_rc,
                                    const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ slot_items,
-                                   int32_t n_slots, int32_t W, double* __restrict__ Hb, double* __restrict__ rhs) {
+                                   int32_t n_slots, int32_t W, double* __restrict__ Hb, double* __restrict__ rhs,
+                                   int32_t nv_band, int32_t nvt, double* __restrict__ BR) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
     const int r0 = slot_rc[2 * s], c0 = slot_rc[2 * s + 1];
@@ -142,7 +145,10 @@ __global__ void gn_assemble_kernel(const double* __restrict__ contrib, const int
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const int R = r0 + r, C = c0 + c;
-            if (C <= R) Hb[static_cast<int64_t>(R) * ld + (R - C)] = blk[r * 3 + c];
+            if (C <= R) {
+                if (R < nv_band) Hb[static_cast<int64_t>(R) * ld + (R - C)] = blk[r * 3 + c];
+                else BR[static_cast<int64_t>(R - nv_band) * nvt + C] = blk[r * 3 + c];
+            }
         }
     if (diag) {
 #pragma unroll
@@ -467,6 +473,118 @@ __global__ __launch_bounds__(kGnBlock) void gn_backsolve_kernel(const double* __
     }
 }
 
+// Band + border: H = [A B; B^T C] with A the band
+// (nv_band scalars, solved by the BCR with mc = 16 ceil((1 + nbd) / 16)
+// right-hand-side columns Z = A^-1 [r_a | B]) and a border of nbd <= 31
+// scalars.  One wave: S = C - B^T Z_B and s = r_b - B^T Z_r over the band rows
+// adjacent to the border (nbr_rows, from the plan: B is zero elsewhere), in a
+// fixed order, then a register Gauss-Jordan of [S | s] (lane c holds column c;
+// pivots and multipliers by v_readlane) -> x_b.
+constexpr int kGnBorderMax = 31;
+constexpr int kGnBorderNbr = 64;   // coupled rows staged per chunk
+__global__ __launch_bounds__(256) void gn_border_solve_kernel(const double* __restrict__ Z, const double* __restrict__ BR,
+                                                             const double* __restrict__ rhs,
+                                                             const int32_t* __restrict__ nbr_rows, int32_t n_nbr,
+                                                             int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc,
+                                                             double* __restrict__ xb, int32_t* __restrict__ status) {
+    __shared__ double M[kGnBorderMax + 1][kGnBorderMax + 2];   // [S | s], row k, column l (l == nbd: s)
+    __shared__ double Bs[kGnBorderNbr][kGnBorderMax + 1];       // B^T columns of the coupled rows (chunk)
+    __shared__ double Zs[kGnBorderNbr][kGnBorderMax + 1];       // Z rows of the coupled rows (chunk)
+    const int tid = threadIdx.x;
+    const int ncol = nbd + 1;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};   // entries e = tid + 256 q of M
+    for (int t0 = 0; t0 < n_nbr; t0 += kGnBorderNbr) {
+        const int nt = min(kGnBorderNbr, n_nbr - t0);
+        __syncthreads();
+        // stage the chunk's rows: every load independent (in flight together)
+        for (int e = tid; e < nt * 32; e += 256) {
+            const int t = e >> 5, k = e & 31;
+            const int R = nbr_rows[t0 + t];
+            Bs[t][k] = k < nbd ? BR[static_cast<int64_t>(k) * nvt + R] : 0.0;
+            Zs[t][k] = k < ncol ? Z[static_cast<int64_t>(R) * mc + (k < nbd ? 1 + k : 0)] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q;
+            if (e < nbd * ncol) {
+                const int k = e / ncol, l = e % ncol;
+                double a = acc[q];
+                for (int t = 0; t < nt; ++t) a = fma(Bs[t][k], Zs[t][l], a);   // fixed order
+                acc[q] = a;
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = tid + 256 * q;
+        if (e < nbd * ncol) {
+            const int k = e / ncol, l = e % ncol;
+            const double v = l < nbd ? (l <= k ? BR[static_cast<int64_t>(k) * nvt + nv_band + l]
+                                               : BR[static_cast<int64_t>(l) * nvt + nv_band + k])
+                                     : rhs[nv_band + k];
+            M[k][l] = v - acc[q];
+        }
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    // [S | s] padded to 32 x 32 with the identity (branch-free, fully unrolled
+    // Gauss-Jordan): lane c < 33 holds column c (c == 32: s)
+    const int lane = tid;
+    double col[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r)
+        col[r] = r < nbd ? (lane < nbd ? M[r][lane] : lane == 32 ? M[r][nbd] : 0.0) : (lane == r ? 1.0 : 0.0);
+    bool bad = false;
+#pragma unroll
+    for (int piv = 0; piv < 32; ++piv) {
+        const double d = readlane_d(col[piv], piv);
+        bad |= !(d > 0.0);
+        const double prow = col[piv] / d;
+#pragma unroll
+        for (int r = 0; r < 32; ++r)
+            if (r != piv) col[r] = fma(-readlane_d(col[r], piv), prow, col[r]);
+        col[piv] = prow;
+    }
+    if (bad && lane == 0) *status = 1;
+    if (lane == 32) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r)
+            if (r < nbd) xb[r] = col[r];
+    }
+}
+
+// The pose update of a bordered solve: dx = [Z_r - Z_B x_b ; x_b], one thread
+// per scalar (its Z row loaded with every load in flight), applied in place.
+template <int MC>
+__global__ void gn_border_update_kernel(double* __restrict__ poses, int32_t N, const int32_t* __restrict__ node_col,
+                                        const double* __restrict__ Z, const double* __restrict__ xb, int32_t nv_band,
+                                        int32_t nbd) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = t / 3, q = t - 3 * n;
+    if (n >= N) return;
+    const int c = node_col[n];
+    if (c < 0) return;
+    const int R = c + q;
+    double d;
+    if (R < nv_band) {
+        const double2* z = reinterpret_cast<const double2*>(Z + static_cast<int64_t>(R) * MC);
+        double2 zr[MC / 2];
+#pragma unroll
+        for (int k = 0; k < MC / 2; ++k) zr[k] = z[k];
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 1; k < MC; ++k) {
+            const double zk = (k & 1) ? zr[k / 2].y : zr[k / 2].x;
+            if (k <= nbd) acc = fma(zk, xb[k - 1], acc);
+        }
+        d = zr[0].x - acc;
+    } else {
+        d = xb[R - nv_band];
+    }
+    poses[3 * n + q] = q == 2 ? wrap_pi(poses[3 * n + 2] + d) : poses[3 * n + q] + d;
+}
+
 __global__ void gn_update_kernel(double* __restrict__ poses, int32_t N, const int32_t* __restrict__ node_col,
                                  const double* __restrict__ dx) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -498,9 +616,10 @@ __global__ __launch_bounds__(1024) void gn_chi2_kernel(const double* __restrict_
 
 namespace slamhip {
 int bcr_block_rows(int32_t nv, int32_t W);
-int64_t bcr_work_size(int32_t nv, int32_t W);
+int64_t bcr_work_size(int32_t nv, int32_t W, int32_t mc);
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
-              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps);
+              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
+              const double* BR, int32_t nbd, int32_t nvt);
 }  // namespace slamhip
 
 using namespace slamhip;
@@ -533,13 +652,22 @@ static int64_t window_dim(int32_t W) {
     return MP;
 }
 
-int64_t slam_gn_work_size(int32_t N, int32_t E, int32_t W) {
+static int gn_border_mc(int32_t nbd) { return nbd > 0 ? 16 * ((nbd + 16) / 16) : 1; }
+
+static int64_t gn_work_size(int32_t N, int32_t E, int32_t W, int32_t nbd) {
     const int64_t nv = 3 * static_cast<int64_t>(N);
     const int64_t MP = window_dim(W);
     const int64_t steps = (nv + kGnS - 1) / kGnS;
     return static_cast<int64_t>(E) * kGnContrib + nv * (W + 1) + nv + MP * (MP + 1) +
            static_cast<int64_t>(kGnS) * lpw(W) + MP + steps * (kGnS + W) * kGnS + 8 +
-           bcr_work_size(static_cast<int32_t>(nv), W) + E;   // last E: per-edge chi2 terms
+           bcr_work_size(static_cast<int32_t>(nv), W, gn_border_mc(nbd)) +
+           (nbd > 0 ? nbd * nv + 32 + nv : 0) + E;   // border rows, x_b, dx; last E: per-edge chi2 terms
+}
+
+int64_t slam_gn_work_size(int32_t N, int32_t E, int32_t W) { return gn_work_size(N, E, W, 0); }
+
+int64_t slam_gn_work_size_bordered(int32_t N, int32_t E, int32_t W, int32_t n_border) {
+    return gn_work_size(N, E, W, n_border);
 }
 
 int slam_gn_max_lds_band(void) {
@@ -553,37 +681,63 @@ int slam_gn_max_lds_band(void) {
     return W;
 }
 
-int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,
-                          const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
-                          const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv,
-                          int32_t W, double* work, double* out_chi2, int32_t* status, void* stream) {
+}  // extern "C"
+
+// One GN iteration; nv_band < nv: the last nv - nv_band scalars are a border
+// (bordered BCR + Schur complement, gn_border_*_kernel).
+static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,
+                        const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
+                        const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv, int32_t W,
+                        int32_t nv_band, const int32_t* nbr_rows, int32_t n_nbr, double* work, double* out_chi2,
+                        int32_t* status, void* stream) {
     if (N < 1 || E < 0 || nv < 0 || W < 2) return fail(SLAM_EINVAL, "gn: N=%d E=%d nv=%d W=%d", N, E, nv, W);
     if (!poses || !ea || !eb || !tf || !w || !node_col || !slot_rc || !slot_ptr || !work || !out_chi2 || !status)
         return fail(SLAM_EINVAL, "gn: null array argument");
+    const int32_t nbd = nv - nv_band;
+    if (nbd < 0 || nbd > kGnBorderMax || (nbd > 0 && n_nbr > 0 && !nbr_rows) || n_nbr < 0)
+        return fail(SLAM_EINVAL, "gn: border of %d scalars (at most %d)", nbd, kGnBorderMax);
     hipStream_t s = as_stream(stream);
     double* contrib = work;
     double* Hb = contrib + static_cast<int64_t>(E) * kGnContrib;
     double* rhs = Hb + static_cast<int64_t>(nv) * (W + 1);
     double* gwin = rhs + nv;
-    double* chi2e = work + slam_gn_work_size(N, E, W) - E;
+    double* chi2e = work + gn_work_size(N, E, W, nbd) - E;
+    const int64_t MPw = window_dim(W);
+    const int64_t steps = (static_cast<int64_t>(nv) + kGnS - 1) / kGnS;
+    double* bwork = gwin + MPw * (MPw + 1) + static_cast<int64_t>(kGnS) * lpw(W) + MPw + steps * (kGnS + W) * kGnS + 8;
+    const int mc = gn_border_mc(nbd);
+    double* BR = bwork + bcr_work_size(3 * N, W, mc);
+    double* xb = BR + static_cast<int64_t>(nbd) * 3 * N;
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, tf, w, E,
                            contrib, chi2e);
     hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, chi2e, E, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
-    if (hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nv) * (W + 1), s) != hipSuccess)
+    if (hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nv_band) * (W + 1), s) != hipSuccess)
+        return fail(SLAM_EHIP, "gn: memset failed");
+    if (nbd > 0 && hipMemsetAsync(BR, 0, sizeof(double) * static_cast<size_t>(nbd) * nv, s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (n_slots > 0)
         hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128), dim3(128), 0, s, contrib, slot_rc,
-                           slot_ptr, slot_items, n_slots, W, Hb, rhs);
-    const int Wb = g_gn_solver == 1 ? 0 : bcr_block_rows(nv, W);
+                           slot_ptr, slot_items, n_slots, W, Hb, rhs, nv_band, nv, BR);
+    const int Wb = g_gn_solver == 1 ? 0 : bcr_block_rows(nv_band, W);
+    if (nbd > 0 && Wb == 0)
+        return fail(SLAM_EINVAL, "gn: a bordered plan needs the cyclic-reduction solver (band %d, %d scalars)", W, nv_band);
     if (Wb > 0) {   // block cyclic reduction: log2(nv / Wb) parallel levels
-        const int64_t MPw = window_dim(W);
-        const int64_t steps = (static_cast<int64_t>(nv) + kGnS - 1) / kGnS;
-        double* bwork = gwin + MPw * (MPw + 1) + static_cast<int64_t>(kGnS) * lpw(W) + MPw + steps * (kGnS + W) * kGnS + 8;
         double* dx = nullptr;
-        const int rc = bcr_solve(Hb, rhs, nv, W, Wb, bwork, &dx, status, s, g_gn_stamps);
+        const int rc = bcr_solve(Hb, rhs, nv_band, W, Wb, bwork, &dx, status, s, g_gn_stamps, mc, BR, nbd, nv);
         if (rc != 0) return rc;
+        if (nbd > 0) {
+            hipLaunchKernelGGL(gn_border_solve_kernel, dim3(1), dim3(256), 0, s, dx, BR, rhs, nbr_rows, n_nbr, nv_band,
+                               nbd, nv, mc, xb, status);
+            if (mc == 16)
+                hipLaunchKernelGGL(gn_border_update_kernel<16>, dim3((3 * N + 255) / 256), dim3(256), 0, s, poses, N,
+                                   node_col, dx, xb, nv_band, nbd);
+            else
+                hipLaunchKernelGGL(gn_border_update_kernel<32>, dim3((3 * N + 255) / 256), dim3(256), 0, s, poses, N,
+                                   node_col, dx, xb, nv_band, nbd);
+            return check_launch("gn kernels");
+        }
         hipLaunchKernelGGL(gn_update_kernel, dim3((N + 255) / 256), dim3(256), 0, s, poses, N, node_col, dx);
         return check_launch("gn kernels");
     }
@@ -618,6 +772,25 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
     }
     hipLaunchKernelGGL(gn_update_kernel, dim3((N + 255) / 256), dim3(256), 0, s, poses, N, node_col, rhs);
     return check_launch("gn kernels");
+}
+
+extern "C" {
+
+int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,
+                          const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
+                          const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv,
+                          int32_t W, double* work, double* out_chi2, int32_t* status, void* stream) {
+    return gn_iteration(poses, N, ea, eb, tf, w, E, node_col, slot_rc, slot_ptr, slot_items, n_slots, nv, W, nv,
+                        nullptr, 0, work, out_chi2, status, stream);
+}
+
+int slam_gn_iteration_bordered_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,
+                                   const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
+                                   const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv,
+                                   int32_t W, int32_t nv_band, const int32_t* nbr_rows, int32_t n_nbr, double* work,
+                                   double* out_chi2, int32_t* status, void* stream) {
+    return gn_iteration(poses, N, ea, eb, tf, w, E, node_col, slot_rc, slot_ptr, slot_items, n_slots, nv, W, nv_band,
+                        nbr_rows, n_nbr, work, out_chi2, status, stream);
 }
 
 }  // extern "C"

@@ -60,6 +60,10 @@ SIGNATURES = {
     "slam_gn_bcr_block_rows": (c_int, [c_int, c_int]),
     "slam_gn_iteration_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                       c_ptr, c_int, c_int, c_int, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "slam_gn_work_size_bordered": (c_i64, [c_int, c_int, c_int, c_int]),
+    "slam_gn_iteration_bordered_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
+                                               c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
+                                               c_ptr]),
 }
 
 

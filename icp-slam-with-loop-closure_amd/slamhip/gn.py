@@ -49,6 +49,12 @@ def place_order(N, ea, eb):
     in pose order, puts a lap edge (p, lap) -> (p + 1, lap) two places apart
     even where RCM over the poses folds the loop unevenly: C4's band is 62
     scalars instead of RCM's 77 (BCR blocks of 64 rows instead of 80)."""
+    nc, lab, Q = _places(N, ea, eb)
+    return _place_major(N, lab, Q, np.ones(nc, dtype=bool))
+
+
+def _places(N, ea, eb):
+    """Places (components of the loop-closure edges) and the place graph."""
     loop = np.abs(eb - ea) != 1
     L = sp.coo_matrix((np.ones(int(loop.sum())), (ea[loop], eb[loop])), shape=(N, N))
     nc, lab = connected_components(L, directed=False)
@@ -56,10 +62,56 @@ def place_order(N, ea, eb):
     x = ca != cb
     Q = sp.coo_matrix((np.ones(2 * int(x.sum()) + nc), (np.r_[ca[x], cb[x], np.arange(nc)],
                                                          np.r_[cb[x], ca[x], np.arange(nc)])), shape=(nc, nc)).tocsr()
-    qo = reverse_cuthill_mckee(Q, symmetric_mode=True)
-    qr = np.empty(nc, dtype=np.int64)
-    qr[qo] = np.arange(nc)
-    return np.lexsort((np.arange(N), qr[lab]))
+    return nc, lab, Q
+
+
+def _place_major(N, lab, Q, keep):
+    """Poses of the kept places, place-major in RCM order of the kept place graph."""
+    idx = np.flatnonzero(keep)
+    qo = idx[reverse_cuthill_mckee(Q[idx][:, idx].tocsr(), symmetric_mode=True)]
+    qr = np.full(len(keep), -1, dtype=np.int64)
+    qr[qo] = np.arange(len(qo))
+    nodes = np.flatnonzero(qr[lab] >= 0)
+    return nodes[np.lexsort((nodes, qr[lab[nodes]]))]
+
+
+MAX_BORDER = 31   # scalars (csrc/gn_kernels.hip kGnBorderMax)
+BCR_MAX_WB = 96   # widest cyclic-reduction block (csrc/gn_bcr.hip kBcrMaxWb); a border needs that solver
+
+
+def border_order(N, ea, eb, fixed=0):
+    """Band + border order for loop trajectories (C4: ten laps of one square).
+
+    The place graph of a lap trajectory is a ring, and any order of a ring
+    folds it (place_order: two places per band step, C4 W = 62).  Taking one
+    place's poses out as a border cuts the ring into a path of places, whose
+    place-major order has a band of one place (C4: W = 32, BCR blocks of 32
+    rows); the border (<= MAX_BORDER scalars) is eliminated by a Schur
+    complement after the band solve (slam_gn_iteration_bordered_f64).  The
+    candidates are the place holding the fixed node and places spread along
+    the ring; returns (order of the band nodes, border nodes, W) of the
+    narrowest band, or None."""
+    ea = np.asarray(ea, dtype=np.int64)
+    eb = np.asarray(eb, dtype=np.int64)
+    if len(ea) == 0:
+        return None
+    nc, lab, Q = _places(N, ea, eb)
+    ring = reverse_cuthill_mckee(Q, symmetric_mode=True)
+    cands = [int(lab[fixed])] + [int(ring[int(f * (nc - 1))]) for f in (0.0, 0.25, 0.5, 0.75)]
+    best = None
+    for c in dict.fromkeys(cands):
+        bnodes = np.flatnonzero((lab == c) & (np.arange(N) != fixed))
+        if len(bnodes) == 0 or 3 * len(bnodes) > MAX_BORDER:
+            continue
+        keep = np.ones(nc, dtype=bool)
+        keep[c] = False
+        if not keep.any():
+            continue
+        band = _place_major(N, lab, Q, keep)
+        w = _band_w(band, ea, eb, N, fixed)
+        if best is None or w < best[2]:
+            best = (band, bnodes, w)
+    return best
 
 
 def band_order(N, ea, eb, fixed=0):
@@ -79,30 +131,60 @@ def band_order(N, ea, eb, fixed=0):
     w = _band_w(po, ea, eb, N, fixed)
     if (w + 15) // 16 < (w_best + 15) // 16 or ((w + 15) // 16 == (w_best + 15) // 16 and w < w_best):
         best = (po, "place-major")
-    return best
+        w_best = w
+    return best + (w_best,)
 
 
 class GnPlan:
     """Symbolic analysis of one graph structure."""
 
-    def __init__(self, N, ea, eb, fixed=0, order=None):
+    def __init__(self, N, ea, eb, fixed=0, order=None, border=None):
+        """order: node order of the band (default: band_order); border: nodes
+        solved as a dense border after the band (default: border_order when
+        its band needs fewer 16-row blocks than the unbordered one; [] none)."""
         ea = np.asarray(ea, dtype=np.int64)
         eb = np.asarray(eb, dtype=np.int64)
         self.N = N
         self.fixed = fixed
-        if order is None:
-            order, self.ordering = band_order(N, ea, eb, fixed)
+        if order is None and border is None:
+            order, self.ordering, w0 = band_order(N, ea, eb, fixed)
+            bo = border_order(N, ea, eb, fixed)
+            wb = (bo[2] + 15) // 16 * 16 if bo is not None else 0
+            if bo is not None and wb < (w0 + 15) // 16 * 16 and wb <= BCR_MAX_WB and \
+                    (3 * N - 3 - 3 * len(bo[1])) // wb >= 4:
+                order, border, self.ordering = bo[0], bo[1], "place-major + border"
+        elif order is None:
+            bset = np.zeros(N, dtype=bool)
+            bset[np.asarray(border, dtype=np.int64)] = True
+            keep = np.flatnonzero(~bset)
+            sub = np.flatnonzero(np.isin(ea, keep) & np.isin(eb, keep))
+            remap = np.full(N, -1, dtype=np.int64)
+            remap[keep] = np.arange(len(keep))
+            o, self.ordering, _ = band_order(len(keep), remap[ea[sub]], remap[eb[sub]], -1)
+            order = keep[o]
+            self.ordering += " + given border"
         else:
             self.ordering = "given"
+        border = np.asarray([] if border is None else border, dtype=np.int64)
+        border = border[border != fixed]
         order = np.asarray(order, dtype=np.int64)
-        order = order[order != fixed]
+        order = order[(order != fixed) & ~np.isin(order, border)]
+        if 3 * len(border) > MAX_BORDER:
+            raise ValueError(f"border of {3 * len(border)} scalars (at most {MAX_BORDER})")
         node_col = np.full(N, -1, dtype=np.int32)
         node_col[order] = 3 * np.arange(len(order), dtype=np.int32)
+        node_col[border] = 3 * (len(order) + np.arange(len(border), dtype=np.int32))
         self.node_col = node_col
-        self.nv = 3 * len(order)
+        self.nv = 3 * (len(order) + len(border))
+        self.nv_band = 3 * len(order)
         ca, cb = node_col[ea], node_col[eb]
-        both = (ca >= 0) & (cb >= 0)
+        both = (ca >= 0) & (cb >= 0) & (ca < self.nv_band) & (cb < self.nv_band)
         self.W = int(max(2, (np.abs(ca[both] - cb[both]).max() + 2) if both.any() else 2))
+        # band rows coupled to the border (B's nonzero rows)
+        xb = (ca >= 0) & (cb >= 0) & ((ca >= self.nv_band) != (cb >= self.nv_band))
+        bn = np.where(ca[xb] < self.nv_band, ca[xb], cb[xb])
+        self.nbr_rows = np.unique((bn[:, None] + np.arange(3)[None, :]).ravel()).astype(np.int32)
+        order = np.r_[order, border]   # every free node in column order (slots below)
 
         # diagonal slots: free node n (in RCM order), items 2e + side (a: 0, b: 1) in
         # edge order; pair slots: one per connected free pair (row = the node with
@@ -183,7 +265,9 @@ class GaussNewton:
         self.slot_rc = dv.to_dev(p.slot_rc, np.int32, dev)
         self.slot_ptr = dv.to_dev(p.slot_ptr, np.int32, dev)
         self.slot_items = dv.to_dev(p.slot_items, np.int32, dev)
-        n = int(_abi.lib().slam_gn_work_size(self.N, self.E, p.W))
+        self.nbr_rows = dv.to_dev(p.nbr_rows if len(p.nbr_rows) else np.zeros(1, np.int32), np.int32, dev)
+        n = int(_abi.lib().slam_gn_work_size_bordered(self.N, self.E, p.W, p.nv - p.nv_band)
+                if p.nv_band < p.nv else _abi.lib().slam_gn_work_size(self.N, self.E, p.W))
         self.work = dv.empty((n,), np.float64, dev)
         self.status = dv.to_dev(np.zeros(1, np.int32), np.int32, dev)
         self.chi2 = None
@@ -193,6 +277,13 @@ class GaussNewton:
     def iterate(self, chi2_out, stream=None):
         """One asynchronous GN iteration; chi2 (before the step) -> chi2_out (device)."""
         p = self.plan
+        if p.nv_band < p.nv:
+            _abi.check(_abi.lib().slam_gn_iteration_bordered_f64(
+                dv.ptr(self.poses), self.N, dv.ptr(self.ea), dv.ptr(self.eb), dv.ptr(self.tf), dv.ptr(self.w),
+                self.E, dv.ptr(self.node_col), dv.ptr(self.slot_rc), dv.ptr(self.slot_ptr), dv.ptr(self.slot_items),
+                p.n_slots, p.nv, p.W, p.nv_band, dv.ptr(self.nbr_rows), len(p.nbr_rows), dv.ptr(self.work),
+                dv.ptr(chi2_out), dv.ptr(self.status), dv.stream_handle(stream)), "slam_gn_iteration_bordered_f64")
+            return
         _abi.check(_abi.lib().slam_gn_iteration_f64(
             dv.ptr(self.poses), self.N, dv.ptr(self.ea), dv.ptr(self.eb), dv.ptr(self.tf), dv.ptr(self.w), self.E,
             dv.ptr(self.node_col), dv.ptr(self.slot_rc), dv.ptr(self.slot_ptr), dv.ptr(self.slot_items),
@@ -295,5 +386,7 @@ def bench_c4(iterations=10, reps=3):
             "gn_graph": f"{len(guess)} nodes / {len(ea)} edges (C4)", "gn_band_W": plan.W,
             "gn_ordering": plan.ordering,
             "gn_plan_s": round(plan_s, 3), "gn_chi2_first_last": [float(chis[0]), float(chis[-1])],
-            "gn_solver": "block cyclic reduction (Wb=%d)" % _abi.lib().slam_gn_bcr_block_rows(plan.nv, plan.W)
-            if _abi.lib().slam_gn_bcr_block_rows(plan.nv, plan.W) > 0 else "band Cholesky"}
+            "gn_border_scalars": plan.nv - plan.nv_band,
+            "gn_solver": "block cyclic reduction (Wb=%d)" % _abi.lib().slam_gn_bcr_block_rows(plan.nv_band, plan.W)
+            + (" + border Schur complement" if plan.nv_band < plan.nv else "")
+            if _abi.lib().slam_gn_bcr_block_rows(plan.nv_band, plan.W) > 0 else "band Cholesky"}

@@ -173,6 +173,29 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea,
                           int32_t nv, int32_t W, double* work,
                           double* out_chi2, int32_t* status, void* stream);
 
+/*
+ * The same iteration for a band + border plan (slamhip/gn.py GnPlan with a
+ * border, e.g. C4's lap graph cut at one place): scalars [0, nv_band) form
+ * the band of half-width W, the last nv - nv_band <= 31 scalars a border
+ * coupled to band rows nbr_rows[0..n_nbr) only.  Solved as H = [A B; B^T C]:
+ * Z = A^-1 [r_a | B] by block cyclic reduction with several right-hand
+ * sides, S = C - B^T Z_B, x_b = S^-1 (r_b - B^T Z_r), x_a = Z_r - Z_B x_b.
+ * work: slam_gn_work_size_bordered(N, E, W, nv - nv_band) doubles.
+ */
+int64_t slam_gn_work_size_bordered(int32_t N, int32_t E, int32_t W,
+                                   int32_t n_border);
+int slam_gn_iteration_bordered_f64(double* poses, int32_t N, const int32_t* ea,
+                                   const int32_t* eb, const double* tf,
+                                   const double* w, int32_t E,
+                                   const int32_t* node_col,
+                                   const int32_t* slot_rc,
+                                   const int32_t* slot_ptr,
+                                   const int32_t* slot_items, int32_t n_slots,
+                                   int32_t nv, int32_t W, int32_t nv_band,
+                                   const int32_t* nbr_rows, int32_t n_nbr,
+                                   double* work, double* out_chi2,
+                                   int32_t* status, void* stream);
+
 /* ---- occupancy grid (src/produce_occupancy_grid.py) ------------------------
  * pts: packed (x, y) scan points, scan_off (S+1), pose4 (S x 4: cos theta,
  * sin theta, x, y of each scan's pose; cos/sin as np.cos/np.sin give them).

@@ -74,15 +74,45 @@ def test_place_major_order_on_c4():
     from slamhip import gn, synthetic
     guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
     N = len(guess)
-    p = gn.GnPlan(N, ea, eb)
-    assert p.ordering == "place-major" and p.W == 62
+    order, name, w = gn.band_order(N, ea, eb)
+    assert name == "place-major" and w == 62
+    assert gn.GnPlan(N, ea, eb, order=order).W == 62
     order = gn.place_order(N, np.asarray(ea, np.int64), np.asarray(eb, np.int64))
     assert sorted(order.tolist()) == list(range(N))
     adj = sp.coo_matrix((np.ones(2 * len(ea)), (np.r_[ea, eb], np.r_[eb, ea])), shape=(N, N)).tocsr()
     assert gn.GnPlan(N, ea, eb, order=reverse_cuthill_mckee(adj, symmetric_mode=True)).W == 77
     # sparse loops (incomplete places): RCM stays
     guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=25, num_loops=3, n_loops=200)
-    assert gn.GnPlan(len(guess), ea, eb).ordering == "rcm"
+    assert gn.band_order(len(guess), ea, eb)[1] == "rcm"
+
+
+def test_border_plan():
+    """Band + border plans: C4 cut at the fixed node's place (27 border
+    scalars, band 32); the border's coupling rows; a given border on a random
+    graph; columns a permutation with the border last."""
+    from slamhip import gn, synthetic
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
+    N = len(guess)
+    p = gn.GnPlan(N, ea, eb)
+    assert p.ordering == "place-major + border" and p.W == 32 and p.nv - p.nv_band == 27
+    cols = p.node_col
+    assert sorted(cols[cols >= 0]) == list(range(0, p.nv, 3)) and cols[0] == -1
+    border = np.flatnonzero(cols >= p.nv_band)
+    assert len(border) == 9 and set(border % 500) == {0}   # the other laps' poses at place 0
+    ea, eb = np.asarray(ea), np.asarray(eb)
+    ca, cb = cols[ea], cols[eb]
+    rows = set()
+    for a, b in zip(ca, cb):
+        if a >= 0 and b >= 0 and (a >= p.nv_band) != (b >= p.nv_band):
+            rows.update(range(min(a, b), min(a, b) + 3))
+    assert sorted(rows) == p.nbr_rows.tolist()
+    band = (ca >= 0) & (cb >= 0) & (ca < p.nv_band) & (cb < p.nv_band)
+    assert np.abs(ca[band] - cb[band]).max() + 2 == p.W
+    guess, ea, eb, tf = _random_graph(90, 30, 5)
+    q = gn.GnPlan(len(guess), ea, eb, border=[3, 17, 44, 60])
+    assert q.nv - q.nv_band == 12 and all(q.node_col[[3, 17, 44, 60]] >= q.nv_band)
+    with pytest.raises(ValueError):
+        gn.GnPlan(len(guess), ea, eb, border=list(range(1, 12)))
 
 
 def test_oracle_converges_on_c4():
@@ -126,15 +156,39 @@ def test_gn_c4_vs_oracle(solver, mode):
     from slamhip import _abi, gn, synthetic
     solver(mode)
     guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
-    if mode == 2:
+    if mode == 2:   # default plan: place-major band of 32 scalars + a 27-scalar border
         p = gn.GnPlan(len(guess), ea, eb)
-        assert _abi.lib().slam_gn_bcr_block_rows(p.nv, p.W) > 0
+        assert p.nv - p.nv_band == 27 and p.W == 32
+        assert _abi.lib().slam_gn_bcr_block_rows(p.nv_band, p.W) > 0
+    else:           # band Cholesky: no border
+        p = gn.GnPlan(len(guess), ea, eb, border=[])
+        assert p.nv == p.nv_band
     ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=5)
-    got, chi = gn.optimize(guess, ea, eb, tf, iterations=5)
+    got, chi = gn.optimize(guess, ea, eb, tf, iterations=5, plan=p)
     assert np.allclose(chi, ref_chi, rtol=1e-8)
     assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
     assert np.abs(go.wrap(got[:, 2] - ref[:, 2])).max() <= 1e-8
     assert chi[-1] < 1e-3 * chi[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("border", [[5], [3, 17, 44, 60], [1, 2, 20, 21, 40, 41, 70, 71, 89, 88]])
+def test_gn_border_random_graph(border):
+    """A given border on a random graph (the band of the rest by RCM / place
+    order, the border solved by the Schur complement after the multi-RHS BCR)
+    against the oracle; the border's scalars take 1, 2 and 3 right-hand-side
+    column tiles' worth of columns (3, 12 and 30 scalars)."""
+    from slamhip import _abi, gn
+    guess, ea, eb, tf = _random_graph(120, 25, 6)
+    p = gn.GnPlan(len(guess), ea, eb, border=border)
+    assert p.nv - p.nv_band == 3 * len(border)
+    if _abi.lib().slam_gn_bcr_block_rows(p.nv_band, p.W) == 0:
+        pytest.skip("band too wide for the cyclic-reduction solver")
+    ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=3)
+    got, chi = gn.optimize(guess, ea, eb, tf, iterations=3, plan=p)
+    assert np.allclose(chi, ref_chi, rtol=1e-9, atol=1e-9)
+    assert np.abs(got[:, :2] - ref[:, :2]).max() <= 1e-8
+    assert np.abs(go.wrap(got[:, 2] - ref[:, 2])).max() <= 1e-8
 
 
 @pytest.mark.gpu
@@ -204,7 +258,7 @@ def test_gn_bcr_block_sizes(shape):
     pps, nl, nloops = shape
     guess, ea, eb, tf, truth = synthetic.lap_graph_c4(poses_per_side=pps, num_loops=nl, n_loops=nloops)
     p = gn.GnPlan(len(guess), ea, eb)
-    Wb = _abi.lib().slam_gn_bcr_block_rows(p.nv, p.W)
+    Wb = _abi.lib().slam_gn_bcr_block_rows(p.nv_band, p.W)
     assert (Wb == 0) == (p.W > 96)
     ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=3)
     got, chi = gn.optimize(guess, ea, eb, tf, iterations=3)

@@ -13,9 +13,9 @@ from slamhip import _abi, gn, synthetic  # noqa: E402
 from slamhip import device as dv  # noqa: E402
 
 
-def timeit(guess, ea, eb, tf, order, label):
+def timeit(guess, ea, eb, tf, order, label, border=None):
     t = dv.torch()
-    plan = gn.GnPlan(len(guess), ea, eb, order=order)
+    plan = gn.GnPlan(len(guess), ea, eb, order=order, border=border)
     s = gn.GaussNewton(guess, ea, eb, tf, plan=plan)
     s.run(2)
     best = 1e9
@@ -25,14 +25,19 @@ def timeit(guess, ea, eb, tf, order, label):
         t0 = time.perf_counter()
         chis = s.run(10)
         best = min(best, time.perf_counter() - t0)
-    wb = _abi.lib().slam_gn_bcr_block_rows(plan.nv, plan.W)
-    print(f"{label:28s} W {plan.W:3d} Wb {wb:3d} {10 / best:8.1f} it/s chi2 {chis[0]:.6g} -> {chis[-1]:.9g}", flush=True)
+    wb = _abi.lib().slam_gn_bcr_block_rows(plan.nv_band, plan.W)
+    print(f"{label:28s} W {plan.W:3d} Wb {wb:3d} border {plan.nv - plan.nv_band:2d} {10 / best:8.1f} it/s "
+          f"chi2 {chis[0]:.6g} -> {chis[-1]:.9g}", flush=True)
 
 
 guess, ea, eb, tf, _ = synthetic.lap_graph_c4()
 N = len(guess)
 per_lap, laps = 500, 10
-timeit(guess, ea, eb, tf, None, "rcm")
+import scipy.sparse as sp  # noqa: E402
+from scipy.sparse.csgraph import reverse_cuthill_mckee  # noqa: E402
+adj = sp.coo_matrix((np.ones(2 * len(ea)), (np.r_[ea, eb], np.r_[eb, ea])), shape=(N, N)).tocsr()
+timeit(guess, ea, eb, tf, None, "default plan")
+timeit(guess, ea, eb, tf, reverse_cuthill_mckee(adj, symmetric_mode=True), "rcm")
 place = np.arange(N) % per_lap
 lap = np.arange(N) // per_lap
 fold = np.where(place < per_lap // 2, 2 * place, 2 * (per_lap - 1 - place) + 1)

@@ -18,5 +18,9 @@ BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc);
 int64_t bcr_gj_work_size(int32_t nv, int32_t Wb, int32_t mc);
 int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_t* status, hipStream_t st);
 int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st);
+// x_b of a bordered solve from the band solution Z (nv_band x mc) and the border rows BR
+int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const int32_t* nbr_rows, int32_t n_nbr,
+                     int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc, double* xb, int32_t* status,
+                     hipStream_t st);
 
 }  // namespace slamhip

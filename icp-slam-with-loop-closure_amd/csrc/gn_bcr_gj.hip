@@ -636,18 +636,20 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
 }
 
 // Bordered solves: x_i = z_i - X_i x_p - Y_i x_n for WB x mc blocks (row
-// stride mc, mc a multiple of 16); x_p and x_n staged in LDS.  Thread t takes
-// row r and 4 consecutive columns per pass (fixed k order: deterministic).
+// stride mc, mc a multiple of 16) as MFMA tiles: x_p, x_n staged in LDS, wave
+// w takes output tiles w, w + 4, ... (fixed k order: deterministic).
 template <int T>
 __global__ __launch_bounds__(kThreads) void back_multi_kernel(const double* __restrict__ Xs,
                                                              const double* __restrict__ Ys,
                                                              const double* __restrict__ bz, double* __restrict__ x,
                                                              int32_t nb, int32_t s, int32_t mc) {
-    constexpr int WB = 16 * T;
+    constexpr int WB = 16 * T, K4 = WB / 4;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* xp = lds;             // [WB][mc]
     double* xn = xp + WB * mc;    // [WB][mc]
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lk = lane >> 4;
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
     const bool hn = n < nb;
@@ -659,23 +661,97 @@ __global__ __launch_bounds__(kThreads) void back_multi_kernel(const double* __re
     __syncthreads();
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
-    const int cq = mc / 4;   // column quads per row
-    for (int e = tid; e < WB * cq; e += kThreads) {
-        const int r = e / cq, c0 = 4 * (e % cq);
-        double a[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int k = 0; k < WB; ++k) {
-            const double xv = X[r * WB + k], yv = hn ? Y[r * WB + k] : 0.0;
-            const double4 u = *reinterpret_cast<const double4*>(xp + k * mc + c0);
-            const double4 v = *reinterpret_cast<const double4*>(xn + k * mc + c0);
-            a[0] = fma(xv, u.x, fma(yv, v.x, a[0]));
-            a[1] = fma(xv, u.y, fma(yv, v.y, a[1]));
-            a[2] = fma(xv, u.z, fma(yv, v.z, a[2]));
-            a[3] = fma(xv, u.w, fma(yv, v.w, a[3]));
-        }
-        const int64_t o = i * RB + r * mc + c0;
+    const int nct = mc / 16;
+    for (int t = wave; t < T * nct; t += 4) {
+        const int ti = t / nct, tc = t - ti * nct;
+        double ax[K4], ay[K4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[o + q] = bz[o + q] - a[q];
+        for (int k4 = 0; k4 < K4; ++k4) {
+            ax[k4] = X[(16 * ti + lr) * WB + 4 * k4 + lk];
+            ay[k4] = hn ? Y[(16 * ti + lr) * WB + 4 * k4 + lk] : 0.0;
+        }
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k4 = 0; k4 < K4; ++k4) {
+            acc = mma(ax[k4], xp[(4 * k4 + lk) * mc + 16 * tc + lr], acc);
+            acc = mma(ay[k4], xn[(4 * k4 + lk) * mc + 16 * tc + lr], acc);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int64_t o = i * RB + (16 * ti + lk + 4 * g) * mc + 16 * tc + lr;
+            x[o] = bz[o] - acc[g];
+        }
+    }
+}
+
+// Border of a bordered solve: S = C - B^T Z_B and
+// s = r_b - B^T Z_r over the band rows coupled to the border (nbr_rows: B is
+// zero elsewhere), staged in chunks with every load in flight and summed in a
+// fixed order; S padded to 32 x 32 with the identity, inverted by the same
+// blocked Gauss-Jordan as the BCR blocks (gj_invert<2>), x_b = S^-1 s.
+constexpr int kBorderMax = 31;
+constexpr int kBorderChunk = 64;
+__global__ __launch_bounds__(kThreads) void border_solve_kernel(const double* __restrict__ Z,
+                                                               const double* __restrict__ BR,
+                                                               const double* __restrict__ rhs,
+                                                               const int32_t* __restrict__ nbr_rows, int32_t n_nbr,
+                                                               int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc,
+                                                               double* __restrict__ xb, int32_t* __restrict__ status) {
+    constexpr int LDA = 33, LDC = 17;
+    __shared__ double A[32 * LDA];
+    __shared__ double C[32 * LDC];
+    __shared__ double sv[32];
+    __shared__ double Bs[kBorderChunk][33];   // B^T columns of the chunk's coupled rows
+    __shared__ double Zs[kBorderChunk][33];   // their Z rows (column 0: Z_r, 1 + k: Z_B)
+    const int tid = threadIdx.x;
+    const int ncol = nbd + 1;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};   // entries e = tid + 256 q of [S | s]
+    for (int t0 = 0; t0 < n_nbr; t0 += kBorderChunk) {
+        const int nt = min(kBorderChunk, n_nbr - t0);
+        __syncthreads();
+        for (int e = tid; e < nt * 32; e += kThreads) {
+            const int t = e >> 5, k = e & 31;
+            const int R = nbr_rows[t0 + t];
+            Bs[t][k] = k < nbd ? BR[static_cast<int64_t>(k) * nvt + R] : 0.0;
+            Zs[t][k] = k < ncol ? Z[static_cast<int64_t>(R) * mc + (k < nbd ? 1 + k : 0)] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + kThreads * q;
+            if (e < nbd * ncol) {
+                const int k = e / ncol, l = e % ncol;
+                double a = acc[q];
+                for (int t = 0; t < nt; ++t) a = fma(Bs[t][k], Zs[t][l], a);
+                acc[q] = a;
+            }
+        }
+    }
+    for (int e = tid; e < 32 * 32; e += kThreads) {   // identity padding
+        const int r = e >> 5, c = e & 31;
+        if (r >= nbd || c >= nbd) A[r * LDA + c] = r == c ? 1.0 : 0.0;
+    }
+    if (tid < 32 && tid >= nbd) sv[tid] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = tid + kThreads * q;
+        if (e < nbd * ncol) {
+            const int k = e / ncol, l = e % ncol;
+            const double v = l < nbd ? (l <= k ? BR[static_cast<int64_t>(k) * nvt + nv_band + l]
+                                               : BR[static_cast<int64_t>(l) * nvt + nv_band + k])
+                                     : rhs[nv_band + k];
+            if (l < nbd) A[k * LDA + l] = v - acc[q];
+            else sv[k] = v - acc[q];
+        }
+    }
+    __syncthreads();
+    const bool bad = gj_invert<2>(A, C);   // ends with a barrier
+    if (bad && tid == 0) *status = 1;
+    if (tid < nbd) {
+        double v = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) v = fma(A[tid * LDA + k], sv[k], v);
+        xb[tid] = v;
     }
 }
 
@@ -778,6 +854,15 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
 }
 
 // Back-substitution, level by level in reverse, after the top kernel wrote x_0.
+int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const int32_t* nbr_rows, int32_t n_nbr,
+                     int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc, double* xb, int32_t* status,
+                     hipStream_t st) {
+    if (nbd < 1 || nbd > bcrgj::kBorderMax) return fail(SLAM_EINVAL, "gn: border of %d scalars", nbd);
+    hipLaunchKernelGGL(bcrgj::border_solve_kernel, dim3(1), dim3(bcrgj::kThreads), 0, st, Z, BR, rhs, nbr_rows, n_nbr,
+                       nv_band, nbd, nvt, mc, xb, status);
+    return check_launch("gn border solve");
+}
+
 int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st) {
     const int nb = (nv + Wb - 1) / Wb;
     using BackFn = void (*)(const double*, const double*, const double*, double*, int32_t, int32_t);

@@ -476,83 +476,8 @@ __global__ __launch_bounds__(kGnBlock) void gn_backsolve_kernel(const double* __
 // Band + border: H = [A B; B^T C] with A the band
 // (nv_band scalars, solved by the BCR with mc = 16 ceil((1 + nbd) / 16)
 // right-hand-side columns Z = A^-1 [r_a | B]) and a border of nbd <= 31
-// scalars.  One wave: S = C - B^T Z_B and s = r_b - B^T Z_r over the band rows
-// adjacent to the border (nbr_rows, from the plan: B is zero elsewhere), in a
-// fixed order, then a register Gauss-Jordan of [S | s] (lane c holds column c;
-// pivots and multipliers by v_readlane) -> x_b.
+// scalars (x_b by bcr_border_solve, gn_bcr_gj.hip).
 constexpr int kGnBorderMax = 31;
-constexpr int kGnBorderNbr = 64;   // coupled rows staged per chunk
-__global__ __launch_bounds__(256) void gn_border_solve_kernel(const double* __restrict__ Z, const double* __restrict__ BR,
-                                                             const double* __restrict__ rhs,
-                                                             const int32_t* __restrict__ nbr_rows, int32_t n_nbr,
-                                                             int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc,
-                                                             double* __restrict__ xb, int32_t* __restrict__ status) {
-    __shared__ double M[kGnBorderMax + 1][kGnBorderMax + 2];   // [S | s], row k, column l (l == nbd: s)
-    __shared__ double Bs[kGnBorderNbr][kGnBorderMax + 1];       // B^T columns of the coupled rows (chunk)
-    __shared__ double Zs[kGnBorderNbr][kGnBorderMax + 1];       // Z rows of the coupled rows (chunk)
-    const int tid = threadIdx.x;
-    const int ncol = nbd + 1;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};   // entries e = tid + 256 q of M
-    for (int t0 = 0; t0 < n_nbr; t0 += kGnBorderNbr) {
-        const int nt = min(kGnBorderNbr, n_nbr - t0);
-        __syncthreads();
-        // stage the chunk's rows: every load independent (in flight together)
-        for (int e = tid; e < nt * 32; e += 256) {
-            const int t = e >> 5, k = e & 31;
-            const int R = nbr_rows[t0 + t];
-            Bs[t][k] = k < nbd ? BR[static_cast<int64_t>(k) * nvt + R] : 0.0;
-            Zs[t][k] = k < ncol ? Z[static_cast<int64_t>(R) * mc + (k < nbd ? 1 + k : 0)] : 0.0;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q;
-            if (e < nbd * ncol) {
-                const int k = e / ncol, l = e % ncol;
-                double a = acc[q];
-                for (int t = 0; t < nt; ++t) a = fma(Bs[t][k], Zs[t][l], a);   // fixed order
-                acc[q] = a;
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int e = tid + 256 * q;
-        if (e < nbd * ncol) {
-            const int k = e / ncol, l = e % ncol;
-            const double v = l < nbd ? (l <= k ? BR[static_cast<int64_t>(k) * nvt + nv_band + l]
-                                               : BR[static_cast<int64_t>(l) * nvt + nv_band + k])
-                                     : rhs[nv_band + k];
-            M[k][l] = v - acc[q];
-        }
-    }
-    __syncthreads();
-    if (tid >= 64) return;
-    // [S | s] padded to 32 x 32 with the identity (branch-free, fully unrolled
-    // Gauss-Jordan): lane c < 33 holds column c (c == 32: s)
-    const int lane = tid;
-    double col[32];
-#pragma unroll
-    for (int r = 0; r < 32; ++r)
-        col[r] = r < nbd ? (lane < nbd ? M[r][lane] : lane == 32 ? M[r][nbd] : 0.0) : (lane == r ? 1.0 : 0.0);
-    bool bad = false;
-#pragma unroll
-    for (int piv = 0; piv < 32; ++piv) {
-        const double d = readlane_d(col[piv], piv);
-        bad |= !(d > 0.0);
-        const double prow = col[piv] / d;
-#pragma unroll
-        for (int r = 0; r < 32; ++r)
-            if (r != piv) col[r] = fma(-readlane_d(col[r], piv), prow, col[r]);
-        col[piv] = prow;
-    }
-    if (bad && lane == 0) *status = 1;
-    if (lane == 32) {
-#pragma unroll
-        for (int r = 0; r < 32; ++r)
-            if (r < nbd) xb[r] = col[r];
-    }
-}
 
 // The pose update of a bordered solve: dx = [Z_r - Z_B x_b ; x_b], one thread
 // per scalar (its Z row loaded with every load in flight), applied in place.
@@ -620,6 +545,9 @@ int64_t bcr_work_size(int32_t nv, int32_t W, int32_t mc);
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
               double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
               const double* BR, int32_t nbd, int32_t nvt);
+int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const int32_t* nbr_rows, int32_t n_nbr,
+                     int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc, double* xb, int32_t* status,
+                     hipStream_t st);
 }  // namespace slamhip
 
 using namespace slamhip;
@@ -728,8 +656,8 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
         const int rc = bcr_solve(Hb, rhs, nv_band, W, Wb, bwork, &dx, status, s, g_gn_stamps, mc, BR, nbd, nv);
         if (rc != 0) return rc;
         if (nbd > 0) {
-            hipLaunchKernelGGL(gn_border_solve_kernel, dim3(1), dim3(256), 0, s, dx, BR, rhs, nbr_rows, n_nbr, nv_band,
-                               nbd, nv, mc, xb, status);
+            const int rb = bcr_border_solve(dx, BR, rhs, nbr_rows, n_nbr, nv_band, nbd, nv, mc, xb, status, s);
+            if (rb != 0) return rb;
             if (mc == 16)
                 hipLaunchKernelGGL(gn_border_update_kernel<16>, dim3((3 * N + 255) / 256), dim3(256), 0, s, poses, N,
                                    node_col, dx, xb, nv_band, nbd);

@@ -320,9 +320,15 @@ __device__ __forceinline__ float box_lb(f32x2 alo, f32x2 ahi, const float4& b) {
 // Skipped candidates have d32 >= lower bound > M2 at the time of the test, and
 // M2 only decreases, so (M1, M2, J1) equal the full scan's.
 constexpr int kSub = 8;
-constexpr int kWin = 4;          // window sub-chunks (32 candidates); 2/5/6/8 measured slower
+#ifndef SLAM_KWIN
+#define SLAM_KWIN 4
+#endif
+#ifndef SLAM_KBATCH
+#define SLAM_KBATCH 3
+#endif
+constexpr int kWin = SLAM_KWIN;  // window sub-chunks (32 candidates); 2/5/6/8 measured slower
 constexpr int kStageUnroll = 4;  // staging loads in flight per thread
-constexpr int kBatch = 3;        // live sub-chunks tested per batch
+constexpr int kBatch = SLAM_KBATCH;   // live sub-chunks tested per batch
 constexpr int kWpe = 4;          // waves/SIMD the default 1081-point instance is compiled for
 
 // Screened distances are non-negative (or +inf), so their IEEE bit patterns
@@ -330,9 +336,9 @@ constexpr int kWpe = 4;          // waves/SIMD the default 1081-point instance i
 // med3 need no NaN canonicalisation of the loop-carried M1, M2).
 // Packed-key top-2 of the window scan (nn_window_pruned): K1 <= K2 the two
 // smallest keys seen.
-constexpr int kWinBits = 5;   // kWin * kSub = 32 window offsets
+constexpr int kWinBits = kWin * kSub <= 16 ? 4 : kWin * kSub <= 32 ? 5 : 6;   // 32 window offsets: 5
 constexpr uint32_t kWinLow = (1u << kWinBits) - 1;
-static_assert(kWin * kSub == 1 << kWinBits, "window offsets fill the key's low bits");
+static_assert(kWin * kSub <= 1 << kWinBits, "window offsets fit the key's low bits");
 // (a & m) | b as ONE v_and_or_b32 (the compiler turns the or of disjoint bits
 // into an add and fuses it with the loop offset: two instructions)
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
@@ -2382,8 +2388,11 @@ static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // unchanged).  Those pairs' sums run over another wave layout: results equal
 // the single launch to rounding (correspondences exact, iterations equal).
 static int g_sched_heads = 64;
-// a full C3 batch (10k pairs) keeps every CU for the bulk: heads there cost ~3 %
-constexpr int kHeadsMaxPairs = 8192;
+// a full C3 batch (10k pairs) keeps every CU for the bulk: heads there cost ~3 %;
+// round 4 (probe 3, profiles/r04_strong_probe.txt): the 5,000-pair shard runs
+// 3.12 ms without the exchange/head tiers and 3.40 ms with them, the 2,500-pair
+// shard 2.84 vs 2.31 ms, so the tiers start below 4,096 pairs
+constexpr int kHeadsMaxPairs = 4096;
 
 static const Instance* pick_head_instance(int max_n1) {
     const Instance* best = nullptr;

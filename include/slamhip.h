@@ -75,7 +75,7 @@ int slam_icp_max_query_points(void);
  *   out_iters int32[B]       number of ICP iterations k (len(transforms) - 1)
  * Stopping rules are the reference's: err < epsilon; iteration > max_iters;
  * |last_err - err| < stopping_thresh from the second iteration on.
- * Batches of >= 2048 pairs run in two phases (slam_icp_set_schedule) with a
+ * Batches of >= 1024 pairs run in two phases (slam_icp_set_schedule) with a
  * transient stream-ordered workspace of 12 B/pair (hipMallocAsync/FreeAsync).
  */
 int slam_icp_batch_f64(const double* pts, const int64_t* scan_off,
@@ -231,7 +231,7 @@ int slam_icp_set_schedule(int probe_iters, int min_pairs);
  * slowest (one per 16 pairs at most) first, on CU-exclusive 512-thread
  * workgroups; the rest runs beside them on a library-owned second stream,
  * joined back before the call's work ends: the strong-scaling tail.  Batches
- * below 8,192 pairs only (a full C3 batch keeps every CU for the bulk).  Sums
+ * below 4,096 pairs only (larger shards keep every CU for the bulk).  Sums
  * are order-free (exact on fixed grids), so results are bit-identical to the
  * single launch.  0 = off; default 64. */
 int slam_icp_set_schedule_heads(int heads);

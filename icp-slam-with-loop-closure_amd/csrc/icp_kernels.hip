@@ -45,7 +45,7 @@ __device__ int g_icp_status;                // nonzero: some pair was outside it
 constexpr int kPairConsts = 34;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab (16 sums + the
                                   // arrival flag; an even count keeps the candidates 16-byte aligned)
 __host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 16 + kPairConsts; }
-enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kBcast = 16 };
+enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kPh0, kPhS, kBcast = 16 };
 
 struct IcpArgs {
     const double2* pts;
@@ -584,6 +584,20 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     lap(2);
 }
 
+// Predicted match of a query without a previous match (the first iteration of a
+// launch): the candidate at the query's bearing in pc2's frame, by linear
+// interpolation over pc2's bearing range (a lidar scan's beams are in bearing
+// order at a fixed step; the rotation of the initial transform shifts the
+// match by as many beams), clamped; the proportional index when pc2 gives no
+// range.  Only the window position depends on it: results do not.
+__device__ __forceinline__ int cold_pred(float fx, float fy, float ph0, float phs, int i, int n1, int n2) {
+    if (phs > 0.0f) {
+        const float j = rintf((atan2f(fy, fx) - ph0) * phs);
+        return static_cast<int>(fminf(fmaxf(j, 0.0f), static_cast<float>(n2 - 1)));
+    }
+    return static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
+}
+
 // Certification of a screened winner.
 // Any candidate at exact squared distance T has screened distance
 // d32 <= F(T) = (1+8u) T + 3a sqrt(T) + 3a^2 (u = 2^-24, a = the coordinate
@@ -825,6 +839,12 @@ __device__ __forceinline__ PairSetup stage_pair(const IcpArgs& a, int n1, int n2
         pconst[kGs2] = gs.m2;
         pconst[kPmax] = pmaxd;
         pconst[kCmax] = cmax;
+        // bearing of pc2's first and last points: a cold query's predicted match
+        // is the candidate at its own bearing (cold_pred), 0 scale = no prediction
+        const double2 f = p2[0], l = p2[n2 - 1];
+        const double ph0 = atan2(f.y, f.x), ph1 = atan2(l.y, l.x);
+        pconst[kPh0] = ph0;
+        pconst[kPhS] = (n2 > 1 && ph1 > ph0) ? static_cast<double>(n2 - 1) / (ph1 - ph0) : 0.0;
     }
     __syncthreads();
     PairSetup r;
@@ -912,6 +932,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     }
 
     if (tid == 0 && part == 0) trace_mark(a, b, 0);
+#ifdef SLAM_ABL_STAGE2X
+    // timing-only ablation: the staging twice (its cost = the difference)
+    (void)stage_pair<BLOCK, SCREEN, PRUNE>(a, n1, n2, p1, p2, resident, cand, candf, box8, red0, red1, pconst);
+#endif
     const PairSetup ps = stage_pair<BLOCK, SCREEN, PRUNE>(a, n1, n2, p1, p2, resident, cand, candf, box8, red0, red1,
                                                           pconst);
     if (tid == 0 && part == 0) trace_mark(a, b, 3);   // staging done (diagnostics)
@@ -1042,8 +1066,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                         for (int k = 0; k < QPT; ++k) {
                             const int i = k * qstride + tid + gshift;
                             const int bp = qprev[k * BLOCK + tid];
-                            pred[k] = bp >= 0 ? bp
-                                                    : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
+                            // (a lane without a query keeps -1: no cold prediction every iteration)
+                            pred[k] = (bp >= 0 || i >= n1) ? max(bp, 0)
+                                                           : cold_pred(fx[k], fy[k], static_cast<float>(pconst[kPh0]),
+                                                          static_cast<float>(pconst[kPhS]), i, n1, n2);
                             vq[k] = i < n1;
                         }
                         // groups holding queries (uniform; only the last can be empty)
@@ -1515,7 +1541,9 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
         float lmin = INFINITY, gfar = INFINITY;
         uint32_t* xb = xbuf + (it & 1) * (kTeam * 4 * 64);
         if (screen) {
-            const int pred = prev >= 0 ? prev : static_cast<int>(static_cast<int64_t>(i) * n2 / max(n1, 1));
+            const int pred = (prev >= 0 || i >= n1) ? max(prev, 0)
+                                                    : cold_pred(fx, fy, static_cast<float>(pconst[kPh0]),
+                                                   static_cast<float>(pconst[kPhS]), i, n1, n2);
             {
                 const int lo = kWin / 2 - ((pred & (kSub - 1)) >= kSub / 2 ? 1 : 0);
                 ws = min(max((pred >> 3) - lo, 0), nsub - kWin);

@@ -82,6 +82,8 @@ def parse():
                    help="W,S: the W slowest-keyed pairs on the wide tier, 1/S of a CU's LDS each (0,1 = off)")
     p.add_argument("--bulk-gangs", default="",
                    help="B,K: batches below B pairs run their bulk as gangs of K workgroups (0,2 = off)")
+    p.add_argument("--sched-warm", type=int, default=-1,
+                   help="1: phase 2 resumes with the saved search state (library default 0)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
     return p.parse_args()
 
@@ -376,6 +378,8 @@ def main():
     if args.bulk_gangs:
         b_, k_ = (int(x) for x in args.bulk_gangs.split(","))
         lib.slam_icp_set_bulk_gangs(b_, k_)
+    if args.sched_warm >= 0:
+        lib.slam_icp_set_schedule_warm(args.sched_warm)
     lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
     batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)

@@ -940,7 +940,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                                                           pconst);
     if (tid == 0 && part == 0) trace_mark(a, b, 3);   // staging done (diagnostics)
     const double cmax = ps.cmax;
-    const double pmaxd = ps.pmaxd;
     const float pmax = ps.pmax;
     const bool screen = ps.screen;
     const int nsub = ps.nsub;
@@ -2042,7 +2041,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
             // the winning chunk: first index reaching the minimum + in-chunk
             // runner-up; its 16 candidate pairs read at once, then two
             // independent chains (even / odd pairs) merged in index order
-            float b1 = INFINITY, b2 = INFINITY;
+            float b2 = INFINITY;   // the winning chunk's runner-up (its minimum is the chunk minimum)
             int j1 = c1 * kChunk;
             {
                 const float4* cp = reinterpret_cast<const float4*>(candf + c1 * kChunk);
@@ -2061,7 +2060,6 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
                 // chain 0 holds offsets {0,1,4,5,...}, chain 1 {2,3,6,7,...}: on a tie
                 // the smaller offset wins (the full scan's first index)
                 const bool one = e1[1] < e1[0] || (e1[1] == e1[0] && ej[1] < ej[0]);
-                b1 = one ? e1[1] : e1[0];
                 j1 += one ? ej[1] : ej[0];
                 b2 = fminf(fmaxf(e1[0], e1[1]), fminf(e2[0], e2[1]));
             }

@@ -104,77 +104,42 @@ __device__ __forceinline__ double quad_bcast(double v, int kq) {
     return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
-// Row kb (0..3, a constant after unrolling) of a wave's four 16-lane rows in
-// every row, by two gfx950 lane-swap ops (v_permlane32_swap: halves, then
-// v_permlane16_swap: row pairs) — no LDS.
-template <int KB>
-__device__ __forceinline__ uint32_t row_bcast_u(uint32_t x) {
-    const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);   // {rows 0 1 0 1, rows 2 3 2 3}
-    const uint32_t y = KB < 2 ? h[0] : h[1];
-    const auto q = __builtin_amdgcn_permlane16_swap(y, y, false, false);   // {row 2a x4, row 2a+1 x4}
-    return (KB & 1) ? q[1] : q[0];
-}
-template <int KB>
-__device__ __forceinline__ double row_bcast_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const uint32_t lo = row_bcast_u<KB>(static_cast<uint32_t>(b)), hi = row_bcast_u<KB>(static_cast<uint32_t>(b >> 32));
-    return __longlong_as_double((static_cast<long long>(hi) << 32) | lo);
-}
-// Lane k (a constant after unrolling) of each 16-lane row in the whole row (DPP row_newbcast).
-template <int K>
-__device__ __forceinline__ double newbcast_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b & 0xffffffff), 0x150 + K, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), 0x150 + K, 0xF, 0xF, false);
-    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
-}
-
 // The 16 x 16 tile at P (row stride LDA) -> its inverse, by ONE wave: a
-// register Gauss-Jordan with lane l holding row r = l & 15, columns
-// 4 (l >> 4) .. + 3 (its 16-lane row cb = l >> 4 holds column block cb of every
-// row).  Per pivot k: the pivot row's entries by DPP row_newbcast of lane k,
-// the pivot column's entry a[r][k] by broadcasting row k >> 2 of the wave
-// (v_permlane32/16_swap), the pivot by v_readlane — every operand by a VALU
-// lane op, no LDS round trip and no barrier on the chain (round 4; was
-// ds_bpermute).  Returns "a pivot was not positive".
-template <int K, int LDA>
-__device__ __forceinline__ void gj_pivot16(double (&v)[4], int r, int cb, bool& bad) {
-    constexpr int KB = K >> 2, KQ = K & 3;
-    const double ark = row_bcast_d<KB>(v[KQ]);     // a[r][k]
-    double akc[4];                                 // a[k][4 cb + q]
-#pragma unroll
-    for (int q = 0; q < 4; ++q) akc[q] = newbcast_d<K>(v[q]);
-    const double akk = readlane_d(v[KQ], 16 * KB + K);
-    bad |= !(akk > 0.0);
-    // reciprocal pivot: v_rcp_f64 and two Newton steps (a few ulp; no fp64
-    // division sequence on the chain)
-    double pv = __builtin_amdgcn_rcp(akk);
-    pv = fma(pv, fma(-akk, pv, 1.0), pv);
-    pv = fma(pv, fma(-akk, pv, 1.0), pv);
-    // one rank-1 update for every entry: with column k's pivot entry taken
-    // as a_kk - 1 and row k's as a_kk + 1, a - u v^T / a_kk gives row k / a_kk,
-    // -column k / a_kk and 1 / a_kk at the pivot (2 selects per pivot)
-    const double u = r == K ? akk - 1.0 : ark;
-    akc[KQ] = cb == KB ? akk + 1.0 : akc[KQ];
-    const double m = u * pv;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = fma(-m, akc[q], v[q]);
-}
-template <int LDA, int K = 0>
-__device__ __forceinline__ void gj_pivots16(double (&v)[4], int r, int cb, bool& bad) {
-    if constexpr (K < 16) {
-        gj_pivot16<K, LDA>(v, r, cb, bad);
-        gj_pivots16<LDA, K + 1>(v, r, cb, bad);
-    }
-}
+// register Gauss-Jordan (lane l: row r = l >> 2, columns c0..c0+3, c0 = 4 (l & 3));
+// per pivot the row-k values come by ds_bpermute from lane 4k + (l & 3), a[r][k]
+// by a DPP quad broadcast, the pivot by v_readlane: no LDS round trip and no
+// barrier on the chain.  Returns "a pivot was not positive".
 template <int LDA>
 __device__ __forceinline__ bool tile_inv16(double* P, int lane) {
-    const int r = lane & 15, cb = lane >> 4, c0 = 4 * cb;
+    const int r = lane >> 2, cq = lane & 3, c0 = 4 * cq;
     bool bad = false;
     double v[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = P[r * LDA + c0 + q];
-    gj_pivots16<LDA>(v, r, cb, bad);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int kq = k >> 2, kr = k & 3;
+        const double ark = quad_bcast(v[kr], kq);
+        const double akk = readlane_d(v[kr], 4 * k + kq);
+        double akc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) akc[q] = bperm_d(v[q], 4 * k + cq);
+        bad |= !(akk > 0.0);
+        // reciprocal pivot: v_rcp_f64 and two Newton steps (a few ulp; no fp64
+        // division sequence on the chain)
+        double pv = __builtin_amdgcn_rcp(akk);
+        pv = fma(pv, fma(-akk, pv, 1.0), pv);
+        pv = fma(pv, fma(-akk, pv, 1.0), pv);
+        // one rank-1 update for every entry: with column k's pivot entry taken
+        // as a_kk - 1 and row k's as a_kk + 1, a - u v^T / a_kk gives row k / a_kk,
+        // -column k / a_kk and 1 / a_kk at the pivot (2 selects per pivot instead
+        // of 8; relative rounding ~a_kk eps on row k)
+        const double u = r == k ? akk - 1.0 : ark;
+        akc[kr] = cq == kq ? akk + 1.0 : akc[kr];
+        const double m = u * pv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fma(-m, akc[q], v[q]);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) P[r * LDA + c0 + q] = v[q];
     return bad;

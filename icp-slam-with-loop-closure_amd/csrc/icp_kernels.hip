@@ -329,10 +329,6 @@ constexpr int kSub = 8;
 constexpr int kWin = SLAM_KWIN;  // window sub-chunks (32 candidates); 2/5/6/8 measured slower
 constexpr int kStageUnroll = 4;  // staging loads in flight per thread
 constexpr int kBatch = SLAM_KBATCH;   // live sub-chunks tested per batch
-#ifndef SLAM_FEW_ACTIVE
-#define SLAM_FEW_ACTIVE 0
-#endif
-constexpr int kFewActive = SLAM_FEW_ACTIVE;   // groups with at most this many active queries: per-query masks
 constexpr int kWpe = 4;          // waves/SIMD the default 1081-point instance is compiled for
 
 // Screened distances are non-negative (or +inf), so their IEEE bit patterns
@@ -495,55 +491,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
     const int nw = (nsub + 63) >> 6;
 #pragma unroll
     for (int k = 0; k < QPT; ++k) {
-        const uint64_t amask = __ballot(act[k]);
-        if (amask == 0) continue;   // wave-uniform
-        if (__popcll(amask) <= kFewActive) {
-            // few active queries (round 4): each one's exact need mask instead of
-            // the group box — its point, M2 and window broadcast (v_readlane),
-            // lane l bounds sub-chunk 64 w + l against that query alone, the
-            // ballot of "outside the window and within M2" is the set its lane
-            // scans, and the smallest bound outside the window its new clearance
-            // radius (tighter than the group box's).  Skipped sub-chunks have
-            // d32 >= bound > M2 as in the group path: the result is the same.
-            uint64_t am = amask;
-            float rq = INFINITY;   // this lane's query: its new clearance bound
-            while (am) {
-                const int src = static_cast<int>(__builtin_ctzll(am));
-                am &= am - 1;
-                const float sx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(qx[k]), src));
-                const float sy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(qy[k]), src));
-                const float sm2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(M2[k]), src));
-                const int sws = __builtin_amdgcn_readlane(ws[k], src);
-                float rmin = INFINITY;
-                for (int w = 0; w < nw; ++w) {
-                    const int sl = 64 * w + lane;
-                    const float lb = box_lb(f32x2{sx, sy}, f32x2{sx, sy}, box8[min(sl, nsub - 1)]);
-                    const bool out = (sl < nsub) & ((sl < sws) | (sl >= sws + kWin));
-                    rmin = out ? fminf(rmin, lb) : rmin;
-                    uint64_t need = __ballot(out & (lb <= sm2));
-                    while (need) {   // rare (0.05-0.12 sub-chunks per group-iteration on C3)
-                        const int c8 = (64 * w + static_cast<int>(__builtin_ctzll(need))) * kSub;
-                        need &= need - 1;
-                        ++nvisit;
-                        if (counting) nev += kSub;
-                        if (lane == src) {
-#pragma unroll
-                            for (int t = 0; t < kSub; t += 2) {
-                                const float4 pp = *reinterpret_cast<const float4*>(candf + c8 + t);
-                                const f32x2v d = screen_pair(pp, qx[k], qy[k]);
-                                take_cand(d.x, c8 + t, M1[k], M2[k], J1[k]);
-                                take_cand(d.y, c8 + t + 1, M1[k], M2[k], J1[k]);
-                            }
-                        }
-                    }
-                }
-                const float r = wave_min_nn(rmin);
-                rq = lane == src ? r : rq;
-            }
-            // lb <= d32 <= (1 + 5u) |q - p|^2, so |q - p| >= sqrt(lb) (1 - 1e-5)
-            if (act[k]) st[k * st_stride] = st_pack(sqrt_bound(rq) * (1.0f - 1e-5f), ws[k]);
-            continue;
-        }
+        if (__ballot(act[k]) == 0) continue;   // wave-uniform
         int g_live = 0, g_vis = 0;   // diagnostics (stamping): this group's live and visited sub-chunks
         unsigned long long f0 = stamping ? __builtin_amdgcn_s_memtime() : 0;
         auto flap = [&](int q) {   // diagnostics: group-loop sub-phases (workgroup 0, wave 0)

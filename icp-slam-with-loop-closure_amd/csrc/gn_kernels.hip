@@ -43,11 +43,20 @@ __device__ __forceinline__ double wrap_pi(double a) {
     return a - 2.0 * M_PI * floor((a + M_PI) / (2.0 * M_PI));
 }
 
+// The same launch zeroes the band (and the border rows) the assembly fills
+// next: grid-stride double2 stores instead of a separate memset launch.
 __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int32_t* __restrict__ ea,
                                     const int32_t* __restrict__ eb, const double* __restrict__ tf,
                                     const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
-                                    double* __restrict__ chi2e) {
+                                    double* __restrict__ chi2e, double2* __restrict__ z0, int64_t nz0,
+                                    double2* __restrict__ z1, int64_t nz1) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    {
+        const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+        const double2 zero = make_double2(0.0, 0.0);
+        for (int64_t q = e; q < nz0; q += stride) z0[q] = zero;
+        for (int64_t q = e; q < nz1; q += stride) z1[q] = zero;
+    }
     if (e >= E) return;
     const int i = ea[e], j = eb[e];
     const double* t = tf + 9 * static_cast<int64_t>(e);
@@ -636,14 +645,20 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
     const int mc = gn_border_mc(nbd);
     double* BR = bwork + bcr_work_size(3 * N, W, mc);
     double* xb = BR + static_cast<int64_t>(nbd) * 3 * N;
+    // the band and the border rows are zeroed by the linearisation launch (an
+    // even number of doubles each: Hb and BR start 16-byte aligned in work)
+    const int64_t nHb = static_cast<int64_t>(nv_band) * (W + 1), nBR = static_cast<int64_t>(nbd) * nv;
+    const bool fold = E > 0 && nHb % 2 == 0 && nBR % 2 == 0 && (reinterpret_cast<uintptr_t>(Hb) & 15) == 0 &&
+                      (reinterpret_cast<uintptr_t>(BR) & 15) == 0;
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, tf, w, E,
-                           contrib, chi2e);
+                           contrib, chi2e, reinterpret_cast<double2*>(Hb), fold ? nHb / 2 : 0,
+                           reinterpret_cast<double2*>(BR), fold ? nBR / 2 : 0);
     hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, chi2e, E, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
-    if (hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nv_band) * (W + 1), s) != hipSuccess)
+    if (!fold && hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nHb), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
-    if (nbd > 0 && hipMemsetAsync(BR, 0, sizeof(double) * static_cast<size_t>(nbd) * nv, s) != hipSuccess)
+    if (!fold && nbd > 0 && hipMemsetAsync(BR, 0, sizeof(double) * static_cast<size_t>(nBR), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (n_slots > 0)
         hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128), dim3(128), 0, s, contrib, slot_rc,

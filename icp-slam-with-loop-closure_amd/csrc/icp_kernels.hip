@@ -2402,7 +2402,13 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
-static int g_sched_probe = 3;          // phase-1 iterations (0: single launch; 3 best on C3 since round 4)
+static int g_sched_probe = -1;   // phase-1 iterations (0: single launch; -1: automatic, sched_probe_for)
+// Automatic probe length (round 4, profiles/r04_probe_shards*.txt, C3 stream):
+// 3 iterations for the full batch (10k pairs: 4.09 ms; 2: 4.11, 4: 4.27) and
+// for 1,250 / 5,000-pair shards; 4 for 2,048-4,095 pairs, where the tail tiers
+// run and a longer probe keys them better (2,500 pairs: 2.03-2.04 ms against
+// 2.14-2.15 with 3; 1,250 pairs: 1.49 against 1.44)
+static int sched_probe_for(int B) { return B >= 2048 && B < 4096 ? 4 : 3; }
 static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // Phase 2 starts the pairs the probe keyed slowest (the top g_sched_heads, at
 // most one per 16 pairs) on workgroups that request the whole LDS of a CU, so
@@ -2673,7 +2679,7 @@ __global__ __launch_bounds__(kSortBlock) void sched_scatter_kernel(const int32_t
 }
 
 static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2, void* stream) {
-    const int probe = g_sched_probe;
+    const int probe = g_sched_probe >= 0 ? g_sched_probe : sched_probe_for(B);
     if (probe <= 0 || B < g_sched_min_pairs || args.max_iters + 2 <= probe)
         return launch(false, args, B, max_n1, max_n2, stream);
     hipStream_t s = as_stream(stream);
@@ -2936,7 +2942,7 @@ int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float
     return rc;
 }
 int slam_icp_set_schedule(int probe_iters, int min_pairs) {
-    if (probe_iters < 0 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: negative argument");
+    if (probe_iters < -1 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: probe_iters < -1 or min_pairs < 0");
     g_sched_probe = probe_iters;
     g_sched_min_pairs = min_pairs;
     return ok();

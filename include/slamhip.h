@@ -224,8 +224,9 @@ int slam_icp_set_screen(int mode);
 /* Phased scheduling of slam_icp_batch_f64 for batches of >= min_pairs pairs:
  * every pair runs probe_iters iterations, then the unfinished ones resume in
  * order of their last error change (slowest-converging first), so the long
- * tail of iteration counts does not start late.  probe_iters = 0: one launch.
- * Defaults (3, 1024).  Results are identical either way. */
+ * tail of iteration counts does not start late.  probe_iters = 0: one launch;
+ * -1 (default): automatic — 3, or 4 for batches of 2,048-4,095 pairs.
+ * Defaults (-1, 1024).  Results are identical either way. */
 int slam_icp_set_schedule(int probe_iters, int min_pairs);
 /* Phase 2 of the scheduler starts the (at most) `heads` pairs the probe keyed
  * slowest (one per 16 pairs at most) first, on CU-exclusive 512-thread

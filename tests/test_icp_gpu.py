@@ -379,7 +379,7 @@ def test_schedule_is_invisible(k):
         assert lib.slam_icp_set_schedule(0, 1) == 0
         ref_ro = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=6, rotation_only=True)
     finally:
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_schedule_heads(64)
     a = outs[0]
     assert a.iters.min() < 8 < a.iters.max()
@@ -409,7 +409,7 @@ def test_default_schedule_large_batch(k):
         assert lib.slam_icp_set_schedule(0, 1024) == 0
         single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
     finally:
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_schedule_heads(64)
     assert phased.iters.max() > 5
     assert np.array_equal(plain.iters, single.iters)
@@ -433,7 +433,7 @@ def test_gangs_are_bit_identical(k):
     try:
         assert lib.slam_icp_set_schedule(0, 1024) == 0
         single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
-        assert lib.slam_icp_set_schedule(3, 1024) == 0
+        assert lib.slam_icp_set_schedule(-1, 1024) == 0
         runs = {}
         for gangs, parts in ((8, 4), (64, 2), (64, 3), (64, 5), (64, 9), (64, 17), (1, 4), (64, 0), (8, 0)):
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
@@ -460,7 +460,7 @@ def test_gangs_are_bit_identical(k):
         ro_single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=7, rotation_only=True)
         assert lib.slam_icp_set_schedule_gangs(1, 1) != 0   # a gang needs two parts
     finally:
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
         lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
@@ -488,7 +488,7 @@ def test_gang_timeouts_are_repaired(k):
     try:
         assert lib.slam_icp_set_schedule(0, 1024) == 0
         single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
-        assert lib.slam_icp_set_schedule(3, 1024) == 0
+        assert lib.slam_icp_set_schedule(-1, 1024) == 0
         assert lib.slam_icp_set_gang_wait(1) == 0
         lib.slam_icp_gang_timeouts()   # clear
         for gangs, parts, wide, bulk in ((64, 4, 0, 0), (16, 0, 0, 0), (0, 4, 16, 0), (8, 4, 0, 2), (0, 4, 0, 3)):
@@ -503,7 +503,7 @@ def test_gang_timeouts_are_repaired(k):
                 assert np.array_equal(h0, h1), (gangs, parts)
     finally:
         lib.slam_icp_set_gang_wait(0)
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
         lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)

@@ -63,7 +63,7 @@ try:
         lib.slam_icp_set_schedule_wide(0, 1)
         print(f"pair {p} iters {its} us/iter (incl. 4 probe iterations on one workgroup) " + " ".join(line), flush=True)
 finally:
-    lib.slam_icp_set_schedule(3, 1024)
+    lib.slam_icp_set_schedule(-1, 1024)
     lib.slam_icp_set_schedule_heads(64)
     lib.slam_icp_set_schedule_gangs(24, 4)
     lib.slam_icp_set_schedule_wide(0, 1)

@@ -49,7 +49,7 @@ def main():
             print(line, flush=True)
             prev = (t, pit)
     finally:
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
 
 
 if __name__ == "__main__":

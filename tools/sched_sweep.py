@@ -76,7 +76,7 @@ def main():
         lib.slam_icp_set_schedule_gangs(24, 4)
         lib.slam_icp_set_schedule_wide(0, 1)
         lib.slam_icp_set_bulk_gangs(0, 2)
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_schedule_warm(1)
 
 

@@ -42,7 +42,7 @@ def main():
                 ts.append(e0.elapsed_time(e1) * 1e3)
             out.append(f"{m} it {np.median(ts):7.1f} us ({np.median(ts) * 256 / P:5.2f} CU-us/pair)")
     finally:
-        lib.slam_icp_set_schedule(3, 1024)
+        lib.slam_icp_set_schedule(-1, 1024)
     print(os.environ.get("SLAMHIP_LIB", "cur"), "; ".join(out), flush=True)
 
 

@@ -46,6 +46,6 @@ try:
         for g in range(parts):
             print(f"   {g:5d} " + " ".join(f"{v:8.0f}" for v in t[g]) + f" {t[g].sum():8.0f}", flush=True)
 finally:
-    lib.slam_icp_set_schedule(3, 1024)
+    lib.slam_icp_set_schedule(-1, 1024)
     lib.slam_icp_set_schedule_gangs(24, 4)
     lib.slam_icp_set_schedule_wide(0, 1)

@@ -1,6 +1,6 @@
 // Phase timing of the explicit-inverse BCR odd kernel (gn_bcr_gj.hip built with
 // SLAM_GJ_STAMPS) on random SPD blocks: one odd block (nb = 3, s = 1) and a
-// C4-sized level (nb = 188, 94 odd blocks), HIP event times and s_memtime
+// C4-sized first level (nb = 469, 234 odd blocks at UB_T = 2), HIP event times and s_memtime
 // cycles of thread 0 of workgroup (0, 0) per phase.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSLAM_GJ_STAMPS \
 //       -I include tools/gj_ubench.hip -o tools/gj_ubench && tools/gj_ubench
@@ -23,12 +23,15 @@ using namespace slamhip;
         }                                                                                      \
     } while (0)
 
-constexpr int T = 5, WB = 16 * T;
+#ifndef UB_T
+#define UB_T 2
+#endif
+constexpr int T = UB_T, WB = 16 * T;   // 2: C4's band + border plan (32-row blocks); 5: 80-row blocks
 
 int main() {
     std::mt19937_64 g(1);
     std::normal_distribution<double> n(0.0, 1.0);
-    for (int nb : {3, 188}) {
+    for (int nb : {3, 469}) {
         std::vector<double> D(static_cast<size_t>(nb) * WB * WB), E(D.size()), bz(static_cast<size_t>(nb) * WB);
         std::vector<double> a(WB * WB);
         for (int i = 0; i < nb; ++i) {
@@ -44,11 +47,11 @@ int main() {
         for (auto& v : bz) v = 0.1 * n(g);
         const size_t B = sizeof(double) * D.size();
         double* work;
-        const int64_t ws = bcr_gj_work_size(nb * WB, WB);
+        const int64_t ws = bcr_gj_work_size(nb * WB, WB, 1);
         CK(hipMalloc(&work, ws * sizeof(double)));
         int32_t* st;
         CK(hipMalloc(&st, 4));
-        const BcrGjBufs b = bcr_gj_bufs(work, nb * WB, WB);
+        const BcrGjBufs b = bcr_gj_bufs(work, nb * WB, WB, 1);
         CK(hipFuncSetAttribute(reinterpret_cast<const void*>(bcrgj::odd_kernel<T>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bcrgj::Lds<T>::bytes)));
         hipEvent_t e0, e1;
@@ -66,7 +69,7 @@ int main() {
             while (cpw < T && n_odd * (2 * ((T + cpw - 1) / cpw) + 1) > 512) ++cpw;
             const int ng = (T + cpw - 1) / cpw;
             hipLaunchKernelGGL(bcrgj::odd_kernel<T>, dim3(n_odd, 2 * ng + 1), dim3(bcrgj::kThreads), bcrgj::Lds<T>::bytes,
-                               0, b.D, b.E0, b.E1, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb, b.SNb, nb, 1, cpw, n_odd, st);
+                               0, b.D, b.E0, b.E1, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb, b.SNb, nb, 1, cpw, n_odd, 1, st);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;

@@ -561,8 +561,8 @@ int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const
 
 using namespace slamhip;
 
-static unsigned long long* g_gn_stamps = nullptr;
-static int g_gn_solver = 0;   // 0 auto, 1 band Cholesky, 2 block cyclic reduction
+static thread_local unsigned long long* g_gn_stamps = nullptr;
+static thread_local int g_gn_solver = 0;   // 0 auto, 1 band Cholesky, 2 block cyclic reduction
 
 extern "C" {
 

@@ -2302,7 +2302,7 @@ static const Instance* pick_instance(int max_n1, int forced) {
     return bestp;
 }
 
-static int g_forced_instance = -1;
+static thread_local int g_forced_instance = -1;
 
 // get_transform + get_error on already-matched rows (src/icp.py:22-52), one
 // workgroup; the same reductions and closed form as the fused kernel.
@@ -2352,10 +2352,10 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
 // NN search mode: 0 exact fp64 scan, 1 fp32 screen (all chunks), 2 fp32
 // screen with exact chunk pruning (default).  Results are identical in all
 // three (tests/test_icp_gpu.py::test_nn_modes_identical).
-static int g_screen = 2;
-static unsigned long long* g_icp_stamps = nullptr;
-static unsigned long long* g_icp_evals = nullptr;
-static unsigned long long* g_icp_trace = nullptr;
+static thread_local int g_screen = 2;
+static thread_local unsigned long long* g_icp_stamps = nullptr;
+static thread_local unsigned long long* g_icp_evals = nullptr;
+static thread_local unsigned long long* g_icp_trace = nullptr;
 
 // inst_override / lds_min: the scheduler's CU-exclusive head launch (below)
 static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2,
@@ -2402,14 +2402,14 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // bit-identical to the single-launch run).
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
-static int g_sched_probe = -1;   // phase-1 iterations (0: single launch; -1: automatic, sched_probe_for)
+static thread_local int g_sched_probe = -1;   // phase-1 iterations (0: single launch; -1: automatic, sched_probe_for)
 // Automatic probe length (round 4, profiles/r04_probe_shards*.txt, C3 stream):
 // 3 iterations for the full batch (10k pairs: 4.09 ms; 2: 4.11, 4: 4.27) and
 // for 1,250 / 5,000-pair shards; 4 for 2,048-4,095 pairs, where the tail tiers
 // run and a longer probe keys them better (2,500 pairs: 2.03-2.04 ms against
 // 2.14-2.15 with 3; 1,250 pairs: 1.49 against 1.44)
 static int sched_probe_for(int B) { return B >= 2048 && B < 4096 ? 4 : 3; }
-static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
+static thread_local int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // Phase 2 starts the pairs the probe keyed slowest (the top g_sched_heads, at
 // most one per 16 pairs) on workgroups that request the whole LDS of a CU, so
 // no other workgroup shares their CU, with an 8-wave instance (a lone pair's
@@ -2419,7 +2419,7 @@ static int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // 1,250-pair shards 3.47 / 3.10 / 2.31 -> 2.88 / 2.41 / 1.79 ms, 10k pairs
 // unchanged).  Those pairs' sums run over another wave layout: results equal
 // the single launch to rounding (correspondences exact, iterations equal).
-static int g_sched_heads = 64;
+static thread_local int g_sched_heads = 64;
 // a full C3 batch (10k pairs) keeps every CU for the bulk: heads there cost ~3 %;
 // round 4 (probe 3, profiles/r04_strong_probe.txt): the 5,000-pair shard runs
 // 3.12 ms without the exchange/head tiers and 3.40 ms with them, the 2,500-pair
@@ -2441,20 +2441,20 @@ static const Instance* pick_head_instance(int max_n1) {
 // which exchange their partial sums every iteration: a lone pair's iteration
 // latency is then one query group's search plus the exchange, not a whole
 // workgroup's.  Results are bit-identical.
-static int g_sched_gangs = 24;
-static int g_sched_gang_parts = 4;
-static uint32_t g_gang_wait = kGangWaitTicks;   // diagnostics can shorten it to force timeouts
+static thread_local int g_sched_gangs = 24;
+static thread_local int g_sched_gang_parts = 4;
+static thread_local uint32_t g_gang_wait = kGangWaitTicks;   // diagnostics can shorten it to force timeouts
 // Wide tier: the top g_sched_wide keyed pairs of a batch below kHeadsMaxPairs
 // run on icp_wide_kernel, one workgroup per 64-query group, each requesting
 // kMaxLds / g_wide_share of LDS (1: CU-exclusive)
-static int g_sched_wide = 0;
-static int g_wide_share = 1;
+static thread_local int g_sched_wide = 0;
+static thread_local int g_wide_share = 1;
 // Bulk gangs: batches of fewer than g_bulk_gang_below pairs run both phases'
 // bulk as gangs of g_bulk_gang_parts workgroups (0 / 1 parts: off)
-static int g_bulk_gang_below = 0;
-static int g_bulk_gang_parts = 2;
+static thread_local int g_bulk_gang_below = 0;
+static thread_local int g_bulk_gang_parts = 2;
 // carry the paused pairs' search state from phase 1 to phase 2 (warm resume)
-static int g_sched_warm = 0;
+static thread_local int g_sched_warm = 0;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {

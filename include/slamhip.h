@@ -19,14 +19,16 @@
  *   - launches are asynchronous and ordered on `stream` (a hipStream_t; NULL
  *     = the legacy default stream) and copy nothing to the host; nothing is
  *     allocated persistently.  One exception to "allocates nothing": a
- *     slam_icp_batch_f64 call of >= 2048 pairs takes a transient
+ *     slam_icp_batch_f64 call of >= 1024 pairs takes a transient
  *     stream-ordered workspace (hipMallocAsync / hipFreeAsync, 12 B per pair),
  *     which stream capture records as graph memory nodes;
  *   - return 0 on success, a negative SLAM_E* code on failure; the message is
  *     available from slam_last_error() (thread-local);
- *   - one host thread per device at a time: the diagnostics switches are
- *     process-global and the batch scheduler's second stream and fork / join
- *     events are one set per device.
+ *   - the tuning and diagnostics switches (slam_icp_set_*, slam_gn_set_*)
+ *     are per host thread (thread-local, like slam_last_error): a thread's
+ *     settings never change another thread's launches;
+ *   - one host thread per device at a time: the batch scheduler's side
+ *     streams and fork / join events are one set per device.
  */
 #ifndef SLAMHIP_H
 #define SLAMHIP_H

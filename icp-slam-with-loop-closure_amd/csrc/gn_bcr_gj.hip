@@ -706,6 +706,17 @@ __global__ __launch_bounds__(kThreads) void border_solve_kernel(const double* __
     const int tid = threadIdx.x;
     const int ncol = nbd + 1;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};   // entries e = tid + 256 q of [S | s]
+    double cv[4] = {0.0, 0.0, 0.0, 0.0};    // their C / r_b values, loaded before the chunks
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = tid + kThreads * q;
+        if (e < nbd * ncol) {
+            const int k = e / ncol, l = e % ncol;
+            cv[q] = l < nbd ? (l <= k ? BR[static_cast<int64_t>(k) * nvt + nv_band + l]
+                                      : BR[static_cast<int64_t>(l) * nvt + nv_band + k])
+                            : rhs[nv_band + k];
+        }
+    }
     for (int t0 = 0; t0 < n_nbr; t0 += kBorderChunk) {
         const int nt = min(kBorderChunk, n_nbr - t0);
         __syncthreads();
@@ -737,11 +748,8 @@ __global__ __launch_bounds__(kThreads) void border_solve_kernel(const double* __
         const int e = tid + kThreads * q;
         if (e < nbd * ncol) {
             const int k = e / ncol, l = e % ncol;
-            const double v = l < nbd ? (l <= k ? BR[static_cast<int64_t>(k) * nvt + nv_band + l]
-                                               : BR[static_cast<int64_t>(l) * nvt + nv_band + k])
-                                     : rhs[nv_band + k];
-            if (l < nbd) A[k * LDA + l] = v - acc[q];
-            else sv[k] = v - acc[q];
+            if (l < nbd) A[k * LDA + l] = cv[q] - acc[q];
+            else sv[k] = cv[q] - acc[q];
         }
     }
     __syncthreads();

@@ -43,19 +43,34 @@ __device__ __forceinline__ double wrap_pi(double a) {
     return a - 2.0 * M_PI * floor((a + M_PI) / (2.0 * M_PI));
 }
 
+// n doubles at z <- 0 by grid-stride double2 stores (a head / tail double by
+// thread 0 when z is not 16-byte aligned or the count is odd)
+__device__ __forceinline__ void zero_doubles(double* __restrict__ z, int64_t n, int64_t t, int64_t stride) {
+    if (n <= 0) return;
+    const int64_t head = (reinterpret_cast<uintptr_t>(z) & 15) ? 1 : 0;
+    const int64_t np = (n - head) / 2;
+    double2* __restrict__ z2 = reinterpret_cast<double2*>(z + head);
+    const double2 zero = make_double2(0.0, 0.0);
+    for (int64_t q = t; q < np; q += stride) z2[q] = zero;
+    if (t == 0) {
+        if (head) z[0] = 0.0;
+        if ((n - head) & 1) z[n - 1] = 0.0;
+    }
+}
+
 // The same launch zeroes the band (and the border rows) the assembly fills
-// next: grid-stride double2 stores instead of a separate memset launch.
+// next, instead of separate memset launches (a memset of an odd number of
+// doubles is two fill kernels).
 __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int32_t* __restrict__ ea,
                                     const int32_t* __restrict__ eb, const double* __restrict__ tf,
                                     const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
-                                    double* __restrict__ chi2e, double2* __restrict__ z0, int64_t nz0,
-                                    double2* __restrict__ z1, int64_t nz1) {
+                                    double* __restrict__ chi2e, double* __restrict__ z0, int64_t nz0,
+                                    double* __restrict__ z1, int64_t nz1) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     {
         const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-        const double2 zero = make_double2(0.0, 0.0);
-        for (int64_t q = e; q < nz0; q += stride) z0[q] = zero;
-        for (int64_t q = e; q < nz1; q += stride) z1[q] = zero;
+        zero_doubles(z0, nz0, e, stride);
+        zero_doubles(z1, nz1, e, stride);
     }
     if (e >= E) return;
     const int i = ea[e], j = eb[e];
@@ -645,15 +660,12 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
     const int mc = gn_border_mc(nbd);
     double* BR = bwork + bcr_work_size(3 * N, W, mc);
     double* xb = BR + static_cast<int64_t>(nbd) * 3 * N;
-    // the band and the border rows are zeroed by the linearisation launch (an
-    // even number of doubles each: Hb and BR start 16-byte aligned in work)
+    // the band and the border rows are zeroed by the linearisation launch
     const int64_t nHb = static_cast<int64_t>(nv_band) * (W + 1), nBR = static_cast<int64_t>(nbd) * nv;
-    const bool fold = E > 0 && nHb % 2 == 0 && nBR % 2 == 0 && (reinterpret_cast<uintptr_t>(Hb) & 15) == 0 &&
-                      (reinterpret_cast<uintptr_t>(BR) & 15) == 0;
+    const bool fold = E > 0;
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, tf, w, E,
-                           contrib, chi2e, reinterpret_cast<double2*>(Hb), fold ? nHb / 2 : 0,
-                           reinterpret_cast<double2*>(BR), fold ? nBR / 2 : 0);
+                           contrib, chi2e, Hb, nHb, BR, nBR);
     hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, chi2e, E, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
     if (!fold && hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nHb), s) != hipSuccess)

@@ -590,23 +590,25 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
     const int p = i - s, n = i + s;
     const bool hn = n < nb;
     const int64_t B2 = static_cast<int64_t>(WB) * WB;
-    for (int k = tid; k < WB; k += kThreads) {
-        xpn[k] = x[static_cast<int64_t>(p) * WB + k];
-        xpn[WB + k] = hn ? x[static_cast<int64_t>(n) * WB + k] : 0.0;
-    }
-    __syncthreads();
     const int tr = tid >> 4, tc = tid & 15;
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
-    // every X / Y load in flight before the first FMA
-    double xv[T][T], yv[T][T];
+    // every X / Y / z load in flight before the x staging and the first FMA
+    double xv[T][T], yv[T][T], zv[T];
 #pragma unroll
-    for (int u = 0; u < T; ++u)
+    for (int u = 0; u < T; ++u) {
 #pragma unroll
         for (int w = 0; w < T; ++w) {
             xv[u][w] = X[(tr + 16 * u) * WB + tc + 16 * w];
             yv[u][w] = hn ? Y[(tr + 16 * u) * WB + tc + 16 * w] : 0.0;
         }
+        zv[u] = tc == 0 ? bz[static_cast<int64_t>(i) * WB + tr + 16 * u] : 0.0;
+    }
+    for (int k = tid; k < WB; k += kThreads) {
+        xpn[k] = x[static_cast<int64_t>(p) * WB + k];
+        xpn[WB + k] = hn ? x[static_cast<int64_t>(n) * WB + k] : 0.0;
+    }
+    __syncthreads();
     double v[T];
 #pragma unroll
     for (int u = 0; u < T; ++u) {
@@ -630,7 +632,7 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
 #pragma unroll
         for (int u = 0; u < T; ++u) {
             const int r = tr + 16 * u;
-            x[static_cast<int64_t>(i) * WB + r] = bz[static_cast<int64_t>(i) * WB + r] - v[u];
+            x[static_cast<int64_t>(i) * WB + r] = zv[u] - v[u];
         }
     }
 }
@@ -654,32 +656,59 @@ __global__ __launch_bounds__(kThreads) void back_multi_kernel(const double* __re
     const int p = i - s, n = i + s;
     const bool hn = n < nb;
     const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
-    for (int e = tid; e < WB * mc; e += kThreads) {
-        xp[e] = x[p * RB + e];
-        xn[e] = hn ? x[n * RB + e] : 0.0;
-    }
-    __syncthreads();
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
     const int nct = mc / 16;
-    for (int t = wave; t < T * nct; t += 4) {
+    // the wave's first tile: its X / Y fragments and z values in flight before
+    // the x staging (the level is a chain of load latencies, not of MFMAs)
+    double ax[K4], ay[K4], zv[4];
+    auto load_tile = [&](int t) {
         const int ti = t / nct, tc = t - ti * nct;
-        double ax[K4], ay[K4];
 #pragma unroll
         for (int k4 = 0; k4 < K4; ++k4) {
             ax[k4] = X[(16 * ti + lr) * WB + 4 * k4 + lk];
             ay[k4] = hn ? Y[(16 * ti + lr) * WB + 4 * k4 + lk] : 0.0;
         }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) zv[g] = bz[i * RB + (16 * ti + lk + 4 * g) * mc + 16 * tc + lr];
+    };
+    if (wave < T * nct) load_tile(wave);
+    {   // x_p, x_n: WB * mc / kThreads (<= 12) values per thread, all loads first
+        constexpr int kMaxPer = 16 * 6 * 32 / kThreads;
+        const int per = WB * mc / kThreads;
+        double vp[kMaxPer], vn[kMaxPer];
+#pragma unroll
+        for (int q = 0; q < kMaxPer; ++q) {
+            const int e = tid + kThreads * q;
+            vp[q] = q < per ? x[p * RB + e] : 0.0;
+            vn[q] = q < per && hn ? x[n * RB + e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kMaxPer; ++q) {
+            const int e = tid + kThreads * q;
+            if (q < per) {
+                xp[e] = vp[q];
+                xn[e] = vn[q];
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = wave; t < T * nct; t += 4) {
+        const int ti = t / nct, tc = t - ti * nct;
         f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k4 = 0; k4 < K4; ++k4) {
             acc = mma(ax[k4], xp[(4 * k4 + lk) * mc + 16 * tc + lr], acc);
             acc = mma(ay[k4], xn[(4 * k4 + lk) * mc + 16 * tc + lr], acc);
         }
+        double zo[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) zo[g] = zv[g];
+        if (t + 4 < T * nct) load_tile(t + 4);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int64_t o = i * RB + (16 * ti + lk + 4 * g) * mc + 16 * tc + lr;
-            x[o] = bz[o] - acc[g];
+            x[o] = zo[g] - acc[g];
         }
     }
 }

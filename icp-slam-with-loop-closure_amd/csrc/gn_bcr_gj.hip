@@ -584,7 +584,6 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
                                                        const double* __restrict__ bz, double* __restrict__ x,
                                                        int32_t nb, int32_t s) {
     constexpr int WB = 16 * T;
-    __shared__ double xpn[2 * WB];
     const int tid = threadIdx.x;
     const int i = s + 2 * s * blockIdx.x;
     const int p = i - s, n = i + s;
@@ -593,8 +592,14 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
     const int tr = tid >> 4, tc = tid & 15;
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
-    // every X / Y / z load in flight before the x staging and the first FMA
-    double xv[T][T], yv[T][T], zv[T];
+    // every X / Y / x_p / x_n / z load in flight before the first FMA (no LDS
+    // staging, no barrier: the level is a chain of load latencies)
+    double xv[T][T], yv[T][T], zv[T], vp[T], vn[T];
+#pragma unroll
+    for (int w = 0; w < T; ++w) {
+        vp[w] = x[static_cast<int64_t>(p) * WB + tc + 16 * w];
+        vn[w] = hn ? x[static_cast<int64_t>(n) * WB + tc + 16 * w] : 0.0;
+    }
 #pragma unroll
     for (int u = 0; u < T; ++u) {
 #pragma unroll
@@ -604,20 +609,14 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
         }
         zv[u] = tc == 0 ? bz[static_cast<int64_t>(i) * WB + tr + 16 * u] : 0.0;
     }
-    for (int k = tid; k < WB; k += kThreads) {
-        xpn[k] = x[static_cast<int64_t>(p) * WB + k];
-        xpn[WB + k] = hn ? x[static_cast<int64_t>(n) * WB + k] : 0.0;
-    }
-    __syncthreads();
     double v[T];
 #pragma unroll
     for (int u = 0; u < T; ++u) {
         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
         for (int w = 0; w < T; ++w) {
-            const int k = tc + 16 * w;
-            a0 = fma(xv[u][w], xpn[k], a0);
-            a1 = fma(yv[u][w], xpn[WB + k], a1);
+            a0 = fma(xv[u][w], vp[w], a0);
+            a1 = fma(yv[u][w], vn[w], a1);
         }
         v[u] = a0 + a1;
     }
@@ -638,17 +637,17 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
 }
 
 // Bordered solves: x_i = z_i - X_i x_p - Y_i x_n for WB x mc blocks (row
-// stride mc, mc a multiple of 16) as MFMA tiles: x_p, x_n staged in LDS, wave
-// w takes output tiles w, w + 4, ... (fixed k order: deterministic).
+// stride mc, mc a multiple of 16) as MFMA tiles, wave w taking output tiles w,
+// w + 4, ... (fixed k order: deterministic).  The level is a chain of load
+// latencies, not of MFMAs: every operand of a tile (X / Y fragments, the x_p /
+// x_n B fragments straight from global memory, z) is loaded at once, with no
+// LDS staging or barrier.
 template <int T>
 __global__ __launch_bounds__(kThreads) void back_multi_kernel(const double* __restrict__ Xs,
                                                              const double* __restrict__ Ys,
                                                              const double* __restrict__ bz, double* __restrict__ x,
                                                              int32_t nb, int32_t s, int32_t mc) {
     constexpr int WB = 16 * T, K4 = WB / 4;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* xp = lds;             // [WB][mc]
-    double* xn = xp + WB * mc;    // [WB][mc]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 15, lk = lane >> 4;
@@ -658,57 +657,31 @@ __global__ __launch_bounds__(kThreads) void back_multi_kernel(const double* __re
     const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
+    const double* xp = x + p * RB;
+    const double* xn = x + n * RB;
     const int nct = mc / 16;
-    // the wave's first tile: its X / Y fragments and z values in flight before
-    // the x staging (the level is a chain of load latencies, not of MFMAs)
-    double ax[K4], ay[K4], zv[4];
-    auto load_tile = [&](int t) {
+    for (int t = wave; t < T * nct; t += 4) {
         const int ti = t / nct, tc = t - ti * nct;
+        double ax[K4], ay[K4], bp[K4], bn[K4], zv[4];
 #pragma unroll
         for (int k4 = 0; k4 < K4; ++k4) {
             ax[k4] = X[(16 * ti + lr) * WB + 4 * k4 + lk];
             ay[k4] = hn ? Y[(16 * ti + lr) * WB + 4 * k4 + lk] : 0.0;
+            bp[k4] = xp[(4 * k4 + lk) * mc + 16 * tc + lr];
+            bn[k4] = hn ? xn[(4 * k4 + lk) * mc + 16 * tc + lr] : 0.0;
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) zv[g] = bz[i * RB + (16 * ti + lk + 4 * g) * mc + 16 * tc + lr];
-    };
-    if (wave < T * nct) load_tile(wave);
-    {   // x_p, x_n: WB * mc / kThreads (<= 12) values per thread, all loads first
-        constexpr int kMaxPer = 16 * 6 * 32 / kThreads;
-        const int per = WB * mc / kThreads;
-        double vp[kMaxPer], vn[kMaxPer];
-#pragma unroll
-        for (int q = 0; q < kMaxPer; ++q) {
-            const int e = tid + kThreads * q;
-            vp[q] = q < per ? x[p * RB + e] : 0.0;
-            vn[q] = q < per && hn ? x[n * RB + e] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < kMaxPer; ++q) {
-            const int e = tid + kThreads * q;
-            if (q < per) {
-                xp[e] = vp[q];
-                xn[e] = vn[q];
-            }
-        }
-    }
-    __syncthreads();
-    for (int t = wave; t < T * nct; t += 4) {
-        const int ti = t / nct, tc = t - ti * nct;
         f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k4 = 0; k4 < K4; ++k4) {
-            acc = mma(ax[k4], xp[(4 * k4 + lk) * mc + 16 * tc + lr], acc);
-            acc = mma(ay[k4], xn[(4 * k4 + lk) * mc + 16 * tc + lr], acc);
+            acc = mma(ax[k4], bp[k4], acc);
+            acc = mma(ay[k4], bn[k4], acc);
         }
-        double zo[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) zo[g] = zv[g];
-        if (t + 4 < T * nct) load_tile(t + 4);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int64_t o = i * RB + (16 * ti + lk + 4 * g) * mc + 16 * tc + lr;
-            x[o] = zo[g] - acc[g];
+            x[o] = zv[g] - acc[g];
         }
     }
 }
@@ -914,8 +887,8 @@ int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStrea
     for (s /= 2; s >= 1; s /= 2) {
         const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
         if (mc > 1)
-            hipLaunchKernelGGL(backms[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads),
-                               2 * sizeof(double) * Wb * mc, st, b.Xs, b.Ys, b.bz, b.x, nb, s, mc);
+            hipLaunchKernelGGL(backms[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bz, b.x,
+                               nb, s, mc);
         else
             hipLaunchKernelGGL(backs[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bz, b.x,
                                nb, s);

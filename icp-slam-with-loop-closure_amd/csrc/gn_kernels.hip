@@ -58,21 +58,10 @@ __device__ __forceinline__ void zero_doubles(double* __restrict__ z, int64_t n, 
     }
 }
 
-// The same launch zeroes the band (and the border rows) the assembly fills
-// next, instead of separate memset launches (a memset of an odd number of
-// doubles is two fill kernels).
-__global__ void gn_linearize_kernel(const double* __restrict__ poses, const int32_t* __restrict__ ea,
-                                    const int32_t* __restrict__ eb, const double* __restrict__ tf,
-                                    const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
-                                    double* __restrict__ chi2e, double* __restrict__ z0, int64_t nz0,
-                                    double* __restrict__ z1, int64_t nz1) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    {
-        const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-        zero_doubles(z0, nz0, e, stride);
-        zero_doubles(z1, nz1, e, stride);
-    }
-    if (e >= E) return;
+// Edge e's residual, Jacobian products (contrib) and chi2 term (returned).
+__device__ __forceinline__ double linearize_edge(const double* __restrict__ poses, const int32_t* __restrict__ ea,
+                                                 const int32_t* __restrict__ eb, const double* __restrict__ tf,
+                                                 const double* __restrict__ w, double* __restrict__ contrib, int e) {
     const int i = ea[e], j = eb[e];
     const double* t = tf + 9 * static_cast<int64_t>(e);
     const double zx = t[2], zy = t[5], zt = atan2(t[3], t[0]);
@@ -123,7 +112,30 @@ __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int3
         o[30 + r] = we * gb;
     }
     o[33] = we * (ev[0] * ev[0] + ev[1] * ev[1] + ev[2] * ev[2]);
-    chi2e[e] = o[33];   // contiguous copy: the chi2 sum reads it coalesced
+    return o[33];
+}
+
+constexpr int kGnLinBlock = 256;   // linearisation threads per workgroup (one chi2 partial each)
+
+// One thread per edge.  The same launch zeroes the band (and the border rows)
+// the assembly fills next, instead of separate memset launches (a memset of
+// an odd number of doubles is two fill kernels), and sums its edges' chi2
+// terms into chi2p[blockIdx.x] (fixed order; the assembly or gn_chi2_kernel
+// adds the partials).
+__global__ __launch_bounds__(kGnLinBlock) void gn_linearize_kernel(
+    const double* __restrict__ poses, const int32_t* __restrict__ ea, const int32_t* __restrict__ eb,
+    const double* __restrict__ tf, const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
+    double* __restrict__ chi2p, double* __restrict__ z0, int64_t nz0, double* __restrict__ z1, int64_t nz1) {
+    __shared__ double red[kGnLinBlock / 64];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    {
+        const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+        zero_doubles(z0, nz0, e, stride);
+        zero_doubles(z1, nz1, e, stride);
+    }
+    double v[1] = {e < E ? linearize_edge(poses, ea, eb, tf, w, contrib, e) : 0.0};
+    block_sum<1, kGnLinBlock / 64>(v, red);
+    if (threadIdx.x == 0) chi2p[blockIdx.x] = v[0];
 }
 
 // Slot s: rows start at scalar r0 = slot_rc[2s], columns at c0 = slot_rc[2s+1].
@@ -133,10 +145,35 @@ __global__ void gn_linearize_kernel(const double* __restrict__ poses, const int3
 // when e's target is the row node (block = (A'WB)^T).
 // Bordered plans: rows R >= nv_band (the border's scalars, ordered last) go to
 // the dense border rows BR[(R - nv_band) * nvt + C] (C <= R) instead of the band.
-__global__ void gn_assemble_kernel(const double* __restrict__ contrib, const int32_t* __restrict__ slot_rc,
-                                   const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ slot_items,
-                                   int32_t n_slots, int32_t W, double* __restrict__ Hb, double* __restrict__ rhs,
-                                   int32_t nv_band, int32_t nvt, double* __restrict__ BR) {
+// chi2 of the partials of gn_linearize_kernel, summed in a fixed order by one
+// workgroup of NT threads
+template <int NT>
+__device__ __forceinline__ void chi2_total(const double* __restrict__ chi2p, int32_t np, double* __restrict__ out,
+                                           double* red) {
+    double q[2] = {0.0, 0.0};
+    int k = threadIdx.x;
+    for (; k + NT < np; k += 2 * NT) {
+        q[0] += chi2p[k];
+        q[1] += chi2p[k + NT];
+    }
+    if (k < np) q[0] += chi2p[k];
+    double v[1] = {q[0] + q[1]};
+    block_sum<1, NT / 64>(v, red);
+    if (threadIdx.x == 0) *out = v[0];
+}
+
+// The launch has one workgroup more than the slots need when out_chi2 is set:
+// it adds the linearisation's chi2 partials beside the assembly.
+__global__ __launch_bounds__(128) void gn_assemble_kernel(
+    const double* __restrict__ contrib, const int32_t* __restrict__ slot_rc, const int32_t* __restrict__ slot_ptr,
+    const int32_t* __restrict__ slot_items, int32_t n_slots, int32_t W, double* __restrict__ Hb,
+    double* __restrict__ rhs, int32_t nv_band, int32_t nvt, double* __restrict__ BR, const double* __restrict__ chi2p,
+    int32_t n_chi2p, double* __restrict__ out_chi2) {
+    if (out_chi2 && blockIdx.x == gridDim.x - 1) {   // uniform
+        __shared__ double red[2];
+        chi2_total<128>(chi2p, n_chi2p, out_chi2, red);
+        return;
+    }
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_slots) return;
     const int r0 = slot_rc[2 * s], c0 = slot_rc[2 * s + 1];
@@ -547,18 +584,11 @@ __global__ void gn_update_kernel(double* __restrict__ poses, int32_t N, const in
 
 // chi2 = sum_e w_e |e_e|^2, deterministic single-block reduction (1024
 // threads, four independent partial sums per thread).
-__global__ __launch_bounds__(1024) void gn_chi2_kernel(const double* __restrict__ chi2e, int32_t E,
-                                                       double* __restrict__ out) {
-    __shared__ double red[16];
-    double q[4] = {0.0, 0.0, 0.0, 0.0};
-    int e = threadIdx.x;
-    for (; e + 3 * 1024 < E; e += 4 * 1024)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] += chi2e[e + u * 1024];
-    for (; e < E; e += 1024) q[0] += chi2e[e];
-    double v[1] = {(q[0] + q[1]) + (q[2] + q[3])};
-    block_sum<1, 16>(v, red);
-    if (threadIdx.x == 0) *out = v[0];
+// chi2 when no assembly runs (no variables or no slots): the partials alone.
+__global__ __launch_bounds__(256) void gn_chi2_kernel(const double* __restrict__ chi2p, int32_t np,
+                                                      double* __restrict__ out) {
+    __shared__ double red[4];
+    chi2_total<256>(chi2p, np, out, red);
 }
 
 }  // namespace slamhip
@@ -663,18 +693,19 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
     // the band and the border rows are zeroed by the linearisation launch
     const int64_t nHb = static_cast<int64_t>(nv_band) * (W + 1), nBR = static_cast<int64_t>(nbd) * nv;
     const bool fold = E > 0;
+    const int n_chi2p = (E + kGnLinBlock - 1) / kGnLinBlock;   // chi2 partials (in chi2e: n_chi2p <= E)
     if (E > 0)
-        hipLaunchKernelGGL(gn_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, ea, eb, tf, w, E,
+        hipLaunchKernelGGL(gn_linearize_kernel, dim3(n_chi2p), dim3(kGnLinBlock), 0, s, poses, ea, eb, tf, w, E,
                            contrib, chi2e, Hb, nHb, BR, nBR);
-    hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(1024), 0, s, chi2e, E, out_chi2);
+    if (nv == 0 || n_slots <= 0) hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(256), 0, s, chi2e, n_chi2p, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
     if (!fold && hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nHb), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (!fold && nbd > 0 && hipMemsetAsync(BR, 0, sizeof(double) * static_cast<size_t>(nBR), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (n_slots > 0)
-        hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128), dim3(128), 0, s, contrib, slot_rc,
-                           slot_ptr, slot_items, n_slots, W, Hb, rhs, nv_band, nv, BR);
+        hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128 + 1), dim3(128), 0, s, contrib, slot_rc,
+                           slot_ptr, slot_items, n_slots, W, Hb, rhs, nv_band, nv, BR, chi2e, n_chi2p, out_chi2);
     const int Wb = g_gn_solver == 1 ? 0 : bcr_block_rows(nv_band, W);
     if (nbd > 0 && Wb == 0)
         return fail(SLAM_EINVAL, "gn: a bordered plan needs the cyclic-reduction solver (band %d, %d scalars)", W, nv_band);

@@ -549,6 +549,7 @@ __global__ void gn_border_update_kernel(double* __restrict__ poses, int32_t N, c
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = t / 3, q = t - 3 * n;
     if (n >= N) return;
+    const double p0 = poses[3 * n + q];   // in flight beside the node_col -> Z chain
     const int c = node_col[n];
     if (c < 0) return;
     const int R = c + q;
@@ -568,22 +569,21 @@ __global__ void gn_border_update_kernel(double* __restrict__ poses, int32_t N, c
     } else {
         d = xb[R - nv_band];
     }
-    poses[3 * n + q] = q == 2 ? wrap_pi(poses[3 * n + 2] + d) : poses[3 * n + q] + d;
+    poses[3 * n + q] = q == 2 ? wrap_pi(p0 + d) : p0 + d;
 }
 
 __global__ void gn_update_kernel(double* __restrict__ poses, int32_t N, const int32_t* __restrict__ node_col,
                                  const double* __restrict__ dx) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
+    const double p0 = poses[3 * n], p1 = poses[3 * n + 1], p2 = poses[3 * n + 2];   // beside the node_col -> dx chain
     const int c = node_col[n];
     if (c < 0) return;
-    poses[3 * n] += dx[c];
-    poses[3 * n + 1] += dx[c + 1];
-    poses[3 * n + 2] = wrap_pi(poses[3 * n + 2] + dx[c + 2]);
+    poses[3 * n] = p0 + dx[c];
+    poses[3 * n + 1] = p1 + dx[c + 1];
+    poses[3 * n + 2] = wrap_pi(p2 + dx[c + 2]);
 }
 
-// chi2 = sum_e w_e |e_e|^2, deterministic single-block reduction (1024
-// threads, four independent partial sums per thread).
 // chi2 when no assembly runs (no variables or no slots): the partials alone.
 __global__ __launch_bounds__(256) void gn_chi2_kernel(const double* __restrict__ chi2p, int32_t np,
                                                       double* __restrict__ out) {

@@ -994,23 +994,30 @@ int64_t bcr_work_size(int32_t nv, int32_t W, int32_t mc) {
 // points at the solution inside `work` (first nv entries).
 // Bordered (mc > 1, explicit-inverse path only): the mc right-hand sides of
 // bcr_load_kernel; *dx_out is then the nv x mc solution block (row stride mc).
-int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
-              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
-              const double* BR, int32_t nbd, int32_t nvt) {
-    const int nb = (nv + Wb - 1) / Wb;
-    const int64_t B2 = bcr_blk(Wb);
-    // default: the explicit-inverse levels (gn_bcr_gj.hip); the Cholesky paths
-    // below stay selectable for A/B (SLAMHIP_BCR_CHOL=1, SLAMHIP_BCR_LEGACY=1)
+// default: the explicit-inverse levels (gn_bcr_gj.hip); the Cholesky paths
+// below stay selectable for A/B (SLAMHIP_BCR_CHOL=1, SLAMHIP_BCR_LEGACY=1)
+bool bcr_gj_default() {
     static const bool chol = [] {
         const char* e = getenv("SLAMHIP_BCR_CHOL");
         const char* l = getenv("SLAMHIP_BCR_LEGACY");
         return (e && e[0] == '1') || (l && l[0] == '1');
     }();
-    if (!chol || mc > 1) {
+    return !chol;
+}
+
+// preloaded: the caller's assembly already wrote the explicit-inverse path's
+// D, E0 and bz (gn_assemble_kernel with a block layout): no load launch.
+int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
+              double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
+              const double* BR, int32_t nbd, int32_t nvt, bool preloaded) {
+    const int nb = (nv + Wb - 1) / Wb;
+    const int64_t B2 = bcr_blk(Wb);
+    if (bcr_gj_default() || mc > 1 || preloaded) {
         const BcrGjBufs g = bcr_gj_bufs(work, nv, Wb, mc);
         const int64_t tot = nb * B2;
-        hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb, rhs,
-                           nv, W, Wb, nb, g.D, g.E0, g.bz, mc, BR, nbd, nvt);
+        if (!preloaded)
+            hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb,
+                               rhs, nv, W, Wb, nb, g.D, g.E0, g.bz, mc, BR, nbd, nvt);
         int rc = bcr_gj_levels(g, nv, Wb, mc, status, st);   // levels + block 0
         if (rc != 0) return rc;
         rc = bcr_gj_back(g, nv, Wb, mc, st);

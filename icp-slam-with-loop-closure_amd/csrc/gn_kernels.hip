@@ -32,6 +32,7 @@
 #include <cstdint>
 
 #include "common.hpp"
+#include "gn_bcr.hpp"
 
 namespace slamhip {
 
@@ -125,13 +126,15 @@ constexpr int kGnLinBlock = 256;   // linearisation threads per workgroup (one c
 __global__ __launch_bounds__(kGnLinBlock) void gn_linearize_kernel(
     const double* __restrict__ poses, const int32_t* __restrict__ ea, const int32_t* __restrict__ eb,
     const double* __restrict__ tf, const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
-    double* __restrict__ chi2p, double* __restrict__ z0, int64_t nz0, double* __restrict__ z1, int64_t nz1) {
+    double* __restrict__ chi2p, double* __restrict__ z0, int64_t nz0, double* __restrict__ z1, int64_t nz1,
+    double* __restrict__ z2, int64_t nz2) {
     __shared__ double red[kGnLinBlock / 64];
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     {
         const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
         zero_doubles(z0, nz0, e, stride);
         zero_doubles(z1, nz1, e, stride);
+        zero_doubles(z2, nz2, e, stride);
     }
     double v[1] = {e < E ? linearize_edge(poses, ea, eb, tf, w, contrib, e) : 0.0};
     block_sum<1, kGnLinBlock / 64>(v, red);
@@ -162,16 +165,34 @@ __device__ __forceinline__ void chi2_total(const double* __restrict__ chi2p, int
     if (threadIdx.x == 0) *out = v[0];
 }
 
+// Block layout of the explicit-inverse cyclic reduction (gn_bcr_gj.hip), filled
+// by the assembly itself when D is set: D_i (Wb x Wb, both triangles, identity
+// past nv_band), E_i = H[i+1, i], and the right-hand sides bz (row stride mc:
+// column 0 the rhs, column 1 + k border column k) — what bcr_load_kernel makes
+// from the band, without its launch.
+struct BcrDirect {
+    double* D;
+    double* E;
+    double* bz;
+    int32_t Wb, mc, nb;
+};
+
 // The launch has one workgroup more than the slots need when out_chi2 is set:
-// it adds the linearisation's chi2 partials beside the assembly.
+// it adds the linearisation's chi2 partials beside the assembly (and writes
+// the identity rows past nv_band of a direct block layout).
 __global__ __launch_bounds__(128) void gn_assemble_kernel(
     const double* __restrict__ contrib, const int32_t* __restrict__ slot_rc, const int32_t* __restrict__ slot_ptr,
     const int32_t* __restrict__ slot_items, int32_t n_slots, int32_t W, double* __restrict__ Hb,
     double* __restrict__ rhs, int32_t nv_band, int32_t nvt, double* __restrict__ BR, const double* __restrict__ chi2p,
-    int32_t n_chi2p, double* __restrict__ out_chi2) {
+    int32_t n_chi2p, double* __restrict__ out_chi2, BcrDirect bd) {
     if (out_chi2 && blockIdx.x == gridDim.x - 1) {   // uniform
         __shared__ double red[2];
         chi2_total<128>(chi2p, n_chi2p, out_chi2, red);
+        if (bd.D) {
+            const int64_t B2 = static_cast<int64_t>(bd.Wb) * bd.Wb;
+            for (int R = nv_band + threadIdx.x; R < bd.nb * bd.Wb; R += blockDim.x)
+                bd.D[(R / bd.Wb) * B2 + static_cast<int64_t>(R % bd.Wb) * (bd.Wb + 1)] = 1.0;
+        }
         return;
     }
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -201,19 +222,38 @@ __global__ __launch_bounds__(128) void gn_assemble_kernel(
         }
     }
     const int ld = W + 1;
+    const int64_t B2 = static_cast<int64_t>(bd.Wb) * bd.Wb;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const int R = r0 + r, C = c0 + c;
             if (C <= R) {
-                if (R < nv_band) Hb[static_cast<int64_t>(R) * ld + (R - C)] = blk[r * 3 + c];
-                else BR[static_cast<int64_t>(R - nv_band) * nvt + C] = blk[r * 3 + c];
+                const double v = blk[r * 3 + c];
+                if (R < nv_band) {
+                    if (bd.D) {   // R - C <= W <= Wb: the same block or the next one
+                        const int bi = R / bd.Wb, rr = R - bi * bd.Wb, bj = C / bd.Wb, cc = C - bj * bd.Wb;
+                        if (bi == bj) {
+                            bd.D[bi * B2 + rr * bd.Wb + cc] = v;
+                            bd.D[bi * B2 + cc * bd.Wb + rr] = v;
+                        } else {
+                            bd.E[bj * B2 + rr * bd.Wb + cc] = v;
+                        }
+                    } else {
+                        Hb[static_cast<int64_t>(R) * ld + (R - C)] = v;
+                    }
+                } else {
+                    BR[static_cast<int64_t>(R - nv_band) * nvt + C] = v;
+                    if (bd.D && C < nv_band) bd.bz[static_cast<int64_t>(C) * bd.mc + 1 + (R - nv_band)] = v;
+                }
             }
         }
     if (diag) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) rhs[r0 + k] = -g[k];
+        for (int k = 0; k < 3; ++k) {
+            rhs[r0 + k] = -g[k];
+            if (bd.D && r0 + k < nv_band) bd.bz[static_cast<int64_t>(r0 + k) * bd.mc] = -g[k];
+        }
     }
 }
 
@@ -598,7 +638,8 @@ int bcr_block_rows(int32_t nv, int32_t W);
 int64_t bcr_work_size(int32_t nv, int32_t W, int32_t mc);
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
               double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
-              const double* BR, int32_t nbd, int32_t nvt);
+              const double* BR, int32_t nbd, int32_t nvt, bool preloaded);
+bool bcr_gj_default();
 int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const int32_t* nbr_rows, int32_t n_nbr,
                      int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc, double* xb, int32_t* status,
                      hipStream_t st);
@@ -690,28 +731,42 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
     const int mc = gn_border_mc(nbd);
     double* BR = bwork + bcr_work_size(3 * N, W, mc);
     double* xb = BR + static_cast<int64_t>(nbd) * 3 * N;
-    // the band and the border rows are zeroed by the linearisation launch
-    const int64_t nHb = static_cast<int64_t>(nv_band) * (W + 1), nBR = static_cast<int64_t>(nbd) * nv;
+    const int Wb = g_gn_solver == 1 ? 0 : bcr_block_rows(nv_band, W);
+    if (nbd > 0 && Wb == 0)
+        return fail(SLAM_EINVAL, "gn: a bordered plan needs the cyclic-reduction solver (band %d, %d scalars)", W, nv_band);
+    // explicit-inverse reduction with edges and slots: the assembly writes its
+    // block layout directly (no band, no load launch)
+    BcrDirect bd{nullptr, nullptr, nullptr, Wb, mc, Wb > 0 ? (nv_band + Wb - 1) / Wb : 0};
+    if (Wb > 0 && nv_band > 0 && E > 0 && n_slots > 0 && bcr_gj_default()) {
+        const BcrGjBufs g = bcr_gj_bufs(bwork, nv_band, Wb, mc);
+        bd.D = g.D;
+        bd.E = g.E0;
+        bd.bz = g.bz;
+    }
+    // the band (or the blocks) and the border rows are zeroed by the linearisation launch
+    const int64_t B2 = static_cast<int64_t>(Wb) * Wb;
+    double* z0 = bd.D ? bd.D : Hb;   // D and E0 are adjacent in the block workspace
+    const int64_t nz0 = bd.D ? 2 * bd.nb * B2 : static_cast<int64_t>(nv_band) * (W + 1);
+    const int64_t nz1 = bd.D ? static_cast<int64_t>(bd.nb) * Wb * mc : 0;
+    const int64_t nBR = static_cast<int64_t>(nbd) * nv;
     const bool fold = E > 0;
     const int n_chi2p = (E + kGnLinBlock - 1) / kGnLinBlock;   // chi2 partials (in chi2e: n_chi2p <= E)
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3(n_chi2p), dim3(kGnLinBlock), 0, s, poses, ea, eb, tf, w, E,
-                           contrib, chi2e, Hb, nHb, BR, nBR);
+                           contrib, chi2e, z0, nz0, bd.bz, nz1, BR, nBR);
     if (nv == 0 || n_slots <= 0) hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(256), 0, s, chi2e, n_chi2p, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
-    if (!fold && hipMemsetAsync(Hb, 0, sizeof(double) * static_cast<size_t>(nHb), s) != hipSuccess)
+    if (!fold && hipMemsetAsync(z0, 0, sizeof(double) * static_cast<size_t>(nz0), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (!fold && nbd > 0 && hipMemsetAsync(BR, 0, sizeof(double) * static_cast<size_t>(nBR), s) != hipSuccess)
         return fail(SLAM_EHIP, "gn: memset failed");
     if (n_slots > 0)
         hipLaunchKernelGGL(gn_assemble_kernel, dim3((n_slots + 127) / 128 + 1), dim3(128), 0, s, contrib, slot_rc,
-                           slot_ptr, slot_items, n_slots, W, Hb, rhs, nv_band, nv, BR, chi2e, n_chi2p, out_chi2);
-    const int Wb = g_gn_solver == 1 ? 0 : bcr_block_rows(nv_band, W);
-    if (nbd > 0 && Wb == 0)
-        return fail(SLAM_EINVAL, "gn: a bordered plan needs the cyclic-reduction solver (band %d, %d scalars)", W, nv_band);
+                           slot_ptr, slot_items, n_slots, W, Hb, rhs, nv_band, nv, BR, chi2e, n_chi2p, out_chi2, bd);
     if (Wb > 0) {   // block cyclic reduction: log2(nv / Wb) parallel levels
         double* dx = nullptr;
-        const int rc = bcr_solve(Hb, rhs, nv_band, W, Wb, bwork, &dx, status, s, g_gn_stamps, mc, BR, nbd, nv);
+        const int rc = bcr_solve(Hb, rhs, nv_band, W, Wb, bwork, &dx, status, s, g_gn_stamps, mc, BR, nbd, nv,
+                                 bd.D != nullptr);
         if (rc != 0) return rc;
         if (nbd > 0) {
             const int rb = bcr_border_solve(dx, BR, rhs, nbr_rows, n_nbr, nv_band, nbd, nv, mc, xb, status, s);

@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -136,6 +137,8 @@ __global__ __launch_bounds__(kGnLinBlock) void gn_linearize_kernel(
         zero_doubles(z1, nz1, e, stride);
         zero_doubles(z2, nz2, e, stride);
     }
+    // workgroups past the edges only zero (the grid is sized for the zeroing)
+    if (static_cast<int64_t>(blockIdx.x) * blockDim.x >= E) return;   // uniform
     double v[1] = {e < E ? linearize_edge(poses, ea, eb, tf, w, contrib, e) : 0.0};
     block_sum<1, kGnLinBlock / 64>(v, red);
     if (threadIdx.x == 0) chi2p[blockIdx.x] = v[0];
@@ -751,8 +754,11 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
     const int64_t nBR = static_cast<int64_t>(nbd) * nv;
     const bool fold = E > 0;
     const int n_chi2p = (E + kGnLinBlock - 1) / kGnLinBlock;   // chi2 partials (in chi2e: n_chi2p <= E)
+    // enough workgroups for the zeroing too (about 16 double2 stores per thread)
+    const int64_t nzero = (nz0 + nz1 + nBR) / 2;
+    const int lin_grid = static_cast<int>(std::max<int64_t>(n_chi2p, std::min<int64_t>((nzero / 16 + kGnLinBlock - 1) / kGnLinBlock, 2048)));
     if (E > 0)
-        hipLaunchKernelGGL(gn_linearize_kernel, dim3(n_chi2p), dim3(kGnLinBlock), 0, s, poses, ea, eb, tf, w, E,
+        hipLaunchKernelGGL(gn_linearize_kernel, dim3(lin_grid), dim3(kGnLinBlock), 0, s, poses, ea, eb, tf, w, E,
                            contrib, chi2e, z0, nz0, bd.bz, nz1, BR, nBR);
     if (nv == 0 || n_slots <= 0) hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(256), 0, s, chi2e, n_chi2p, out_chi2);
     if (nv == 0) return check_launch("gn kernels");

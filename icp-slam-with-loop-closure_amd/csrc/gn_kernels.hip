@@ -15,8 +15,11 @@
 //   gn_assemble_kernel    one thread per H block slot (free node diagonal or
 //                         connected node pair), summing its edge list in a
 //                         fixed order -> deterministic, no atomics; writes the
-//                         lower band of H (nodes in reverse Cuthill-McKee order,
-//                         half-bandwidth W scalars) and the right-hand side
+//                         lower band of H (nodes in the plan's order,
+//                         half-bandwidth W scalars) and the right-hand side —
+//                         or, for the default explicit-inverse cyclic
+//                         reduction (gn_bcr_gj.hip), H's blocks in that
+//                         solver's layout directly
 //   gn_factor_kernel      ONE workgroup: blocked right-looking band Cholesky,
 //                         the active (W + S) x (W + S) window resident in LDS,
 //                         L overwrites H in place

@@ -207,7 +207,46 @@ __global__ __launch_bounds__(128) void gn_assemble_kernel(
     double blk[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     double g[3] = {0, 0, 0};
     const bool diag = r0 == c0;
-    for (int p = slot_ptr[s]; p < slot_ptr[s + 1]; ++p) {
+    int p = slot_ptr[s];
+    const int pe = slot_ptr[s + 1];
+    // items four at a time: their indices, then all their contributions in
+    // flight, then the sums in item order (the same order as one at a time);
+    // the rest one at a time (a masked last batch measured slower)
+    constexpr int kU = 4;
+    for (; p + kU <= pe; p += kU) {
+        int it[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) it[u] = slot_items[p + u];
+        double q[kU][9], q3[kU][3];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const double* o = contrib + static_cast<int64_t>(it[u] >> 1) * kGnContrib;
+            const int base = diag ? ((it[u] & 1) ? 18 : 0) : 9;
+            const int go = (it[u] & 1) ? 30 : 27;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) q[u][k] = o[base + k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) q3[u][k] = diag ? o[go + k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (diag) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) blk[k] += q[u][k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] += q3[u][k];
+            } else if (it[u] & 1) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) blk[r * 3 + c] += q[u][c * 3 + r];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) blk[k] += q[u][k];
+            }
+        }
+    }
+    for (; p < pe; ++p) {
         const int it = slot_items[p];
         const double* o = contrib + static_cast<int64_t>(it >> 1) * kGnContrib;
         if (diag) {

@@ -531,9 +531,21 @@ __global__ __launch_bounds__(kThreads) void top_kernel(const double* __restrict_
         // behind vz, row stride mc + 1); each thread sums whole dot products
         double* R = vz + 2 * WB;
         const int64_t RB = static_cast<int64_t>(WB) * mc;
-        for (int e = tid; e < WB * mc; e += kThreads) {
-            const int r = e / mc, c = e % mc;
-            R[r * (mc + 1) + c] = sl > 0 ? bz[e] - SPb[sl * RB + e] : bz[e];
+        {   // all loads first (WB * mc / kThreads <= 12 per thread), then the stores
+            constexpr int kMaxPer = 16 * 6 * 32 / kThreads;
+            const int per = WB * mc / kThreads;
+            double bv[kMaxPer], sv[kMaxPer];
+#pragma unroll
+            for (int q = 0; q < kMaxPer; ++q) {
+                const int e = tid + kThreads * q;
+                bv[q] = q < per ? bz[e] : 0.0;
+                sv[q] = q < per && sl > 0 ? SPb[sl * RB + e] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < kMaxPer; ++q) {
+                const int e = tid + kThreads * q;
+                if (q < per) R[(e / mc) * (mc + 1) + e % mc] = sl > 0 ? bv[q] - sv[q] : bv[q];
+            }
         }
         __syncthreads();
         const bool bad = gj_invert<T>(A, C);
@@ -722,11 +734,30 @@ __global__ __launch_bounds__(kThreads) void border_solve_kernel(const double* __
     for (int t0 = 0; t0 < n_nbr; t0 += kBorderChunk) {
         const int nt = min(kBorderChunk, n_nbr - t0);
         __syncthreads();
-        for (int e = tid; e < nt * 32; e += kThreads) {
-            const int t = e >> 5, k = e & 31;
-            const int R = nbr_rows[t0 + t];
-            Bs[t][k] = k < nbd ? BR[static_cast<int64_t>(k) * nvt + R] : 0.0;
-            Zs[t][k] = k < ncol ? Z[static_cast<int64_t>(R) * mc + (k < nbd ? 1 + k : 0)] : 0.0;
+        {   // every row index, then every B / Z value in flight, then the LDS stores
+            constexpr int kPer = kBorderChunk * 32 / kThreads;
+            int rv[kPer];
+            double bv[kPer], zv[kPer];
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const int e = tid + kThreads * q;
+                rv[q] = e < nt * 32 ? nbr_rows[t0 + (e >> 5)] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const int e = tid + kThreads * q, k = e & 31;
+                const bool in = e < nt * 32;
+                bv[q] = in && k < nbd ? BR[static_cast<int64_t>(k) * nvt + rv[q]] : 0.0;
+                zv[q] = in && k < ncol ? Z[static_cast<int64_t>(rv[q]) * mc + (k < nbd ? 1 + k : 0)] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const int e = tid + kThreads * q;
+                if (e < nt * 32) {
+                    Bs[e >> 5][e & 31] = bv[q];
+                    Zs[e >> 5][e & 31] = zv[q];
+                }
+            }
         }
         __syncthreads();
 #pragma unroll

@@ -714,6 +714,8 @@ int slam_gn_set_solver(int mode) {
     return ok();
 }
 
+int slam_gn_get_solver(void) { return g_gn_solver; }
+
 static int64_t window_dim(int32_t W) {
     int64_t MP = 32;
     while (MP < W + kGnS) MP <<= 1;

@@ -2589,7 +2589,13 @@ constexpr int kNB = kSchedBuckets + 1;   // buckets incl. "finished"
 constexpr int kScanChunk = 32;           // blocks per LDS chunk of the scan (32 KB)
 
 __device__ __forceinline__ int sched_bucket(const int32_t* iters, const float* key, int b, float thresh) {
-    if (iters[b] > 0) return kSchedBuckets;   // finished pairs go last (their workgroups exit at once)
+    const int s = iters[b];
+    // finished and out-of-bounds pairs go last (their workgroups exit at once)
+    if (s > 0 || s == kBadBounds) return kSchedBuckets;
+    // not started (a phase-1 bulk gang that timed out left out_iters 0 and no
+    // key): it has every iteration ahead of it, so it goes first; the key is
+    // read only for paused pairs, which wrote it
+    if (s == 0) return 0;
     const float l = log2f(fmaxf(key[b] / thresh, 1e-30f));   // 8 buckets per octave, 2^16 -> 0
     return min(max(static_cast<int>(floorf(128.0f - 8.0f * l)), 0), kSchedBuckets - 1);
 }

@@ -53,6 +53,7 @@ SIGNATURES = {
     "slam_gn_max_lds_band": (c_int, []),
     "slam_gn_set_stamps": (c_int, [c_ptr]),
     "slam_gn_set_solver": (c_int, [c_int]),
+    "slam_gn_get_solver": (c_int, []),
     "slam_grid_work_size": (c_i64, [c_int, c_int, c_int]),
     "slam_grid_global_points_f64": (c_int, [c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "slam_grid_update_i8": (c_int, [c_ptr, c_ptr, c_int, c_ptr, c_i64, c_dbl, c_dbl, c_dbl, c_int, c_int, c_int,

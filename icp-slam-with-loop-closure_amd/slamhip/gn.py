@@ -118,15 +118,15 @@ def band_order(N, ea, eb, fixed=0):
     """Node order for the band solvers: reverse Cuthill-McKee over the poses
     or the place-major order (place_order), whichever gives the narrower band
     (the BCR cost grows with the band rounded up to 16 rows).  Returns
-    (order, name)."""
+    (order, name, W)."""
     ea = np.asarray(ea, dtype=np.int64)
     eb = np.asarray(eb, dtype=np.int64)
     adj = sp.coo_matrix((np.ones(2 * len(ea) + N), (np.r_[ea, eb, np.arange(N)], np.r_[eb, ea, np.arange(N)])),
                         shape=(N, N)).tocsr()
     best = (reverse_cuthill_mckee(adj, symmetric_mode=True), "rcm")
-    if len(ea) == 0:
-        return best
     w_best = _band_w(best[0], ea, eb, N, fixed)
+    if len(ea) == 0:
+        return best + (w_best,)
     po = place_order(N, ea, eb)
     w = _band_w(po, ea, eb, N, fixed)
     if (w + 15) // 16 < (w_best + 15) // 16 or ((w + 15) // 16 == (w_best + 15) // 16 and w < w_best):
@@ -138,15 +138,21 @@ def band_order(N, ea, eb, fixed=0):
 class GnPlan:
     """Symbolic analysis of one graph structure."""
 
-    def __init__(self, N, ea, eb, fixed=0, order=None, border=None):
+    def __init__(self, N, ea, eb, fixed=0, order=None, border=None, allow_border=None):
         """order: node order of the band (default: band_order); border: nodes
         solved as a dense border after the band (default: border_order when
-        its band needs fewer 16-row blocks than the unbordered one; [] none)."""
+        its band needs fewer 16-row blocks than the unbordered one; [] none).
+        allow_border (default: unless slam_gn_set_solver(1) forces the band
+        Cholesky, which takes no border) gates the default border."""
         ea = np.asarray(ea, dtype=np.int64)
         eb = np.asarray(eb, dtype=np.int64)
         self.N = N
         self.fixed = fixed
-        if order is None and border is None:
+        if allow_border is None:
+            allow_border = _border_allowed()
+        if order is None and border is None and not allow_border:
+            order, self.ordering, _ = band_order(N, ea, eb, fixed)
+        elif order is None and border is None:
             order, self.ordering, w0 = band_order(N, ea, eb, fixed)
             bo = border_order(N, ea, eb, fixed)
             wb = (bo[2] + 15) // 16 * 16 if bo is not None else 0
@@ -228,6 +234,15 @@ class GnPlan:
         self.n_slots = len(rc)
 
 
+def _border_allowed():
+    """A default border needs the cyclic-reduction solver: not while the
+    band Cholesky is forced (slam_gn_set_solver(1))."""
+    try:
+        return int(_abi.lib().slam_gn_get_solver()) != 1
+    except (OSError, AttributeError):
+        return True
+
+
 _PLANS = {}   # structure -> GnPlan (a pipeline re-optimises the same graph structure)
 
 
@@ -236,12 +251,13 @@ def plan_for(N, ea, eb, fixed=0):
     order, band width, slot lists) depends only on (N, edge endpoints, fixed)."""
     ea = np.ascontiguousarray(ea, dtype=np.int32)
     eb = np.ascontiguousarray(eb, dtype=np.int32)
-    key = (int(N), int(fixed), ea.tobytes(), eb.tobytes())
+    allow = _border_allowed()
+    key = (int(N), int(fixed), allow, ea.tobytes(), eb.tobytes())
     p = _PLANS.get(key)
     if p is None:
         if len(_PLANS) >= 8:
             _PLANS.pop(next(iter(_PLANS)))
-        p = _PLANS[key] = GnPlan(N, ea, eb, fixed)
+        p = _PLANS[key] = GnPlan(N, ea, eb, fixed, allow_border=allow)
     return p
 
 

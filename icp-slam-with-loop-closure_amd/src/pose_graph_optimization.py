@@ -16,6 +16,8 @@ with their signatures and in-place semantics:
 New: ``optimize_pose_graph`` — the Gauss-Newton solve (J^T J assembly +
 Cholesky on the GPU) named by this build's north star; see slamhip.gn.
 """
+import warnings
+
 import numpy as np
 
 from slamhip import icp as _icp
@@ -107,7 +109,10 @@ def gn_measurements(pose_graph, odometry_edges="global_delta", loop_edges="icp")
     its shape, PER EDGE: (a, a+1) is a constructor delta at the current pose's
     heading, any other edge follows ``loop_edges``.  So an unannotated pickle
     that later gets closures added with a convention keeps its odometry
-    edges as deltas."""
+    edges as deltas.  The shape rule applies only while NO edge carries a
+    heading: in a graph whose constructor edges are annotated, a bare
+    (a, a+1) edge is a constraint saved without its convention (an older
+    pickle of this build) and follows ``loop_edges``, with a warning."""
     if odometry_edges not in ("global_delta", "relative") or loop_edges not in ("icp", "relative"):
         raise ValueError("odometry_edges in {global_delta, relative}, loop_edges in {icp, relative}")
     ea, eb, tf = pose_graph.edge_arrays() if hasattr(pose_graph, "edge_arrays") else _edges(pose_graph)
@@ -118,9 +123,18 @@ def gn_measurements(pose_graph, odometry_edges="global_delta", loop_edges="icp")
         head, conv, added = np.full(len(ea), np.nan), np.zeros(len(ea), np.int8), np.zeros(len(ea), bool)
     delta = ~np.isnan(head)
     bare = ~delta & ~added & (conv == 0) & (eb.astype(np.int64) == ea.astype(np.int64) + 1)
-    if bare.any():   # unannotated (a, a+1): the shape rule, at the current heading
+    if bare.any() and not delta.any():
+        # a graph with no heading annotation anywhere (the reference's own
+        # PoseGraph or pickle): unannotated (a, a+1) edges are constructor
+        # deltas, at the current heading (the shape rule)
         head = np.where(bare, np.asarray(pose_graph.poses, dtype=np.float64)[ea, 2], head)
         delta = delta | bare
+    elif bare.any():
+        # a mixed graph: its constructor edges carry headings, so a bare
+        # (a, a+1) edge is a constraint whose convention was not recorded (an
+        # older pickle of this build); it follows loop_edges, as it did there
+        warnings.warn(f"{int(bare.sum())} unannotated (a, a+1) edge(s) in a graph whose odometry edges carry "
+                      f"headings: treated as loop constraints (loop_edges={loop_edges!r})", stacklevel=2)
     if odometry_edges == "global_delta" and delta.any():
         th = head[delta]
         c, s = np.cos(th), np.sin(th)

@@ -282,9 +282,14 @@ int slam_icp_set_gang_wait(uint32_t ticks);
 int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float thresh, int32_t* order,
                         void* stream);
 int slam_gn_set_stamps(void* dev_buf);
-/* GN linear solver: 0 auto (block cyclic reduction when the band allows it),
- * 1 band Cholesky, 2 block cyclic reduction (falls back to 1 if not allowed). */
+/* GN linear solver (per host thread): 0 auto (block cyclic reduction when the
+ * band allows it), 1 band Cholesky, 2 block cyclic reduction (falls back to 1
+ * if the band is too wide).  A bordered plan (slam_gn_iteration_bordered_f64)
+ * needs the cyclic-reduction solver: with mode 1, or a band too wide for it,
+ * that entry point returns SLAM_EINVAL; slamhip.gn plans without a border
+ * while mode 1 is set (slam_gn_get_solver). */
 int slam_gn_set_solver(int mode);
+int slam_gn_get_solver(void);
 /* Block rows of the cyclic-reduction solver for (nv, W), 0 = not applicable. */
 int slam_gn_bcr_block_rows(int32_t nv, int32_t W);
 /* Diagnostics: per-phase s_memtime totals of workgroup 0 into a device buffer of

@@ -46,6 +46,15 @@ def reference_grid_functions():
     return ns
 
 
+def numpy_build():
+    """NumPy version and BLAS library (name, version, architecture): the
+    build whose matmul rounding grid_ref.npz pins (tests/test_occupancy.py)."""
+    from threadpoolctl import threadpool_info
+    blas = sorted(f"{i.get('internal_api')}-{i.get('version')}-{i.get('architecture')}"
+                  for i in threadpool_info() if i.get("user_api") == "blas")
+    return f"numpy {np.__version__}; blas {','.join(blas)}"
+
+
 def pack(arrs):
     off = np.zeros(len(arrs) + 1, dtype=np.int64)
     off[1:] = np.cumsum([len(a) for a in arrs])
@@ -81,6 +90,9 @@ def main():
     pts, off = pack(seq.scans)
     out.update(upd_poses=seq.truth.copy(), upd_pts=pts, upd_off=off, upd_grid=g1)
     out["n_cases"] = np.array(len(cases))
+    # the reference's global points come from a per-point NumPy 3x3 @ 3x1
+    # product whose rounding depends on the BLAS kernel: record the build
+    out["numpy_build"] = np.array(numpy_build())
     np.savez_compressed(os.path.join(HERE, "grid_ref.npz"), **out)
     print("wrote grid_ref.npz:", {k: v.shape for k, v in out.items() if k.startswith("grid") or k == "upd_grid"})
 

@@ -160,9 +160,10 @@ def test_gn_c4_vs_oracle(solver, mode):
         p = gn.GnPlan(len(guess), ea, eb)
         assert p.nv - p.nv_band == 27 and p.W == 32
         assert _abi.lib().slam_gn_bcr_block_rows(p.nv_band, p.W) > 0
-    else:           # band Cholesky: no border
-        p = gn.GnPlan(len(guess), ea, eb, border=[])
+    else:           # band Cholesky: the default plan takes no border under mode 1
+        p = gn.plan_for(len(guess), ea, eb)
         assert p.nv == p.nv_band
+        assert gn.GnPlan(len(guess), ea, eb, allow_border=True).nv > p.nv_band
     ref, ref_chi = go.optimize(guess, ea, eb, tf, iterations=5)
     got, chi = gn.optimize(guess, ea, eb, tf, iterations=5, plan=p)
     assert np.allclose(chi, ref_chi, rtol=1e-8)
@@ -410,6 +411,41 @@ def test_unannotated_pickle_plus_annotated_closures(tmp_path):
     assert chi2(q, loop_edges="icp") > 1e-8
 
 
+def test_older_pickle_bare_constraint_in_annotated_graph_warns(tmp_path):
+    """An older pickle of this build: constructor edges annotated with their
+    headings, and an add_constraint (a, a+1) edge saved before the
+    ``constraint`` flag existed (heading popped, no convention).  The shape
+    rule does not apply in a graph that carries headings: the bare edge
+    follows loop_edges, with a warning."""
+    import warnings
+
+    import src.pose_graph as pgm
+    import src.pose_graph_optimization as pgo
+    from slamhip import se2, synthetic
+    s = synthetic.make_loop_sequence(200, seed=5, n_beams=31)
+    X = [se2.pose_to_mat(p) for p in s.truth]
+    q = pgm.PoseGraph(s.truth.copy())
+    q.add_constraint(20, 21, np.linalg.inv(X[20]) @ X[21])    # relative: X_21 = X_20 T
+    del q.graph.edges[20, 21]["constraint"]                   # as an older pickle stored it
+    q._flat = None
+
+    def chi2(**kw):
+        ea, eb, z = pgo.gn_measurements(q, **kw)
+        return go.build_system(s.truth.copy(), ea.astype(np.int64), eb.astype(np.int64),
+                               go.edge_measurements(z), go.information(ea, eb))[3]
+    with pytest.warns(UserWarning, match="unannotated"):
+        assert chi2(loop_edges="relative") < 1e-20
+    with pytest.warns(UserWarning):
+        assert chi2(loop_edges="icp") > 1e-8
+    # a fully unannotated graph: no warning, the shape rule
+    for _, _, d in q.graph.edges(data=True):
+        d.pop("heading", None)
+    q._flat = None
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        pgo.gn_measurements(q)
+
+
 def test_edge_arrays_cache_invalidate():
     """Edits that keep the edge count are not seen by the cache;
     PoseGraph.invalidate() drops it (and the drop-in SGD solver keyed on it)."""
@@ -563,3 +599,31 @@ def test_plan_matches_loop_construction(case):
     order = np.argsort(np.where(p.node_col >= 0, p.node_col, np.iinfo(np.int32).max), kind="stable")[:p.nv // 3]
     rc, ptr, items = _loop_plan_slots(N, np.asarray(ea), np.asarray(eb), p.node_col, order)
     assert np.array_equal(p.slot_rc, rc) and np.array_equal(p.slot_ptr, ptr) and np.array_equal(p.slot_items, items)
+
+
+def test_plan_without_edges():
+    """A graph without edges (one pose, or poses not yet linked) plans: the
+    band order's early exit returns its width too."""
+    from slamhip import gn
+    p = gn.GnPlan(1, [], [])
+    assert p.nv == 0 and p.n_slots == 0
+    q = gn.GnPlan(4, np.zeros(0, np.int64), np.zeros(0, np.int64), allow_border=True)
+    assert q.nv == 9 and q.W == 2 and q.nv == q.nv_band
+    order, name, w = gn.band_order(4, [], [])
+    assert sorted(order.tolist()) == [0, 1, 2, 3] and w == 2
+
+
+def test_plan_border_gated_by_solver_mode():
+    """Under slam_gn_set_solver(1) (band Cholesky, no border) the default plan
+    has no border; mode 0 restores the bordered C4 plan."""
+    from slamhip import _abi, gn, synthetic
+    lib = _abi.lib()
+    guess, ea, eb, tf, _ = synthetic.lap_graph_c4()
+    try:
+        assert lib.slam_gn_set_solver(1) == 0 and lib.slam_gn_get_solver() == 1
+        p1 = gn.plan_for(len(guess), ea, eb)
+        assert p1.nv == p1.nv_band
+    finally:
+        lib.slam_gn_set_solver(0)
+    p0 = gn.plan_for(len(guess), ea, eb)
+    assert p0.nv - p0.nv_band == 27 and p0 is not p1

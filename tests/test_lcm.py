@@ -1,23 +1,18 @@
 """LCM log input (§8(f4), reference src/dataloader.py + src/lcmtypes): the
 build's vectorised decoder against the reference's own LCM type code (the
 fixture's messages were encoded and decoded by it, tests/golden/gen_lcm.py),
-and the point-cloud conversion / odometry alignment restated from
-src/dataloader.py:47-55, :83-107 (that module imports cv2 and lcm, absent)."""
+and the point-cloud conversion and both branches of the time alignment
+against the reference's own ``get_point_cloud`` / ``align_data``
+(tests/golden/dataloader_ref.npz, made by gen_dataloader.py, which runs those
+two functions extracted from src/dataloader.py with ``ast``: the module
+imports cv2 and lcm, absent here).  The event-log framing itself is the LCM
+library's (absent): it is checked against the build's own writer only."""
 import os
 
 import numpy as np
 import pytest
 
 from conftest import GOLDEN
-
-
-def _ref_point_cloud(ranges, thetas):
-    """src/dataloader.py:47-55, restated."""
-    r = np.array(ranges).reshape((-1, 1))
-    th = -np.array(thetas).reshape((-1, 1))
-    keep = 0.05 < r
-    r, th = r[keep], th[keep]
-    return np.hstack(((r * np.cos(th)).reshape((-1, 1)), (r * np.sin(th)).reshape((-1, 1))))
 
 
 def test_codecs_match_reference_fixture():
@@ -41,20 +36,98 @@ def test_codecs_match_reference_fixture():
     assert lcmlog.decode_lidar(lcmlog.encode_lidar(ut, r, th))[0] == ut
 
 
-def test_parse_lcm_log_vs_restated_reference():
+def _ref_clouds(d):
+    off = d["cloud_off"]
+    return [d["cloud_pts"][off[k]:off[k + 1]] for k in range(len(off) - 1)]
+
+
+def test_point_cloud_vs_reference(golden):
+    """get_point_cloud equals the reference's function bit for bit: the lidar
+    scans of the fixture log and the 0.05 m cut (exactly 0.05 dropped)."""
     import src.dataloader as dl
+    d = golden("dataloader_ref.npz")
     e = np.load(os.path.join(GOLDEN, "lcm_expected.npz"))
-    odometry, clouds = dl.parse_lcm_log(os.path.join(GOLDEN, "lcm_run"), load_images=False)
     off = e["off"]
-    assert len(clouds) == len(off) - 1
-    for k, c in enumerate(clouds):
-        ref = _ref_point_cloud(e["ranges"][off[k]:off[k + 1]], e["thetas"][off[k]:off[k + 1]])
-        assert np.array_equal(c, ref)
-    for k in range(len(clouds)):   # align_data, no-image branch
-        i = np.searchsorted(e["odo_t"].astype(float), float(e["lid_t"][k]))
-        assert np.array_equal(odometry[k], e["odo"][i if i < len(e["odo"]) else -1])
-    with pytest.raises(NotImplementedError):
-        dl.parse_lcm_log(os.path.join(GOLDEN, "lcm_run"), load_images=True)
+    for k, ref in enumerate(_ref_clouds(d)):
+        assert np.array_equal(dl.get_point_cloud(e["ranges"][off[k]:off[k + 1]].tolist(),
+                                                 e["thetas"][off[k]:off[k + 1]].tolist()), ref), k
+    got = dl.get_point_cloud(d["cut_ranges"], d["cut_thetas"])
+    assert got.shape == (3, 2) and np.array_equal(got, d["cut_cloud"])
+
+
+def test_parse_lcm_log_without_images_vs_reference(golden):
+    """parse_lcm_log(load_images=False): the reference's align_data no-image
+    branch (odometry at every scan time)."""
+    import src.dataloader as dl
+    d = golden("dataloader_ref.npz")
+    odometry, clouds = dl.parse_lcm_log(os.path.join(GOLDEN, "lcm_run"), load_images=False)
+    ref = _ref_clouds(d)
+    assert len(clouds) == len(ref) and all(np.array_equal(c, r) for c, r in zip(clouds, ref))
+    assert np.array_equal(odometry, d["noimg_odometry"])
+
+
+def test_parse_lcm_log_with_images_vs_reference(golden):
+    """parse_lcm_log(load_images=True), what scripts/main.py:226 calls: three
+    values; odometry and scans sampled at the camera times of
+    image_timestamps.txt exactly as the reference's align_data image branch
+    does (times before, on, between and past the records); the frames are a
+    lazy sequence (OpenCV only when pixels are read)."""
+    import src.dataloader as dl
+    d = golden("dataloader_ref.npz")
+    folder = os.path.join(GOLDEN, "lcm_run")
+    odometry, clouds, images = dl.parse_lcm_log(folder, load_images=True, image_stop=np.inf, n_jobs=-1)
+    ref = _ref_clouds(d)
+    assert np.array_equal(odometry, d["img_odometry"])
+    assert len(clouds) == len(d["img_cloud_index"])
+    for c, k in zip(clouds, d["img_cloud_index"]):
+        assert np.array_equal(c, ref[k])
+    assert len(images) == len(d["img_timestamps"]) == images.shape[0]
+    _, ts = dl.get_images(folder, np.inf, -1)
+    assert np.array_equal(ts, d["img_timestamps"])
+    # image_stop (main.py passes --dataset-end): frames 0..image_stop
+    o4, c4, im4 = dl.parse_lcm_log(folder, load_images=True, image_stop=3)
+    assert len(im4) == 4 and np.array_equal(o4, d["img4_odometry"])
+    assert all(np.array_equal(c, ref[k]) for c, k in zip(c4, d["img4_cloud_index"]))
+    # image_stop == len(lines): the reference indexes past the file, and so does this
+    with pytest.raises(IndexError):
+        dl.get_images(folder, len(d["img_timestamps"]), -1)
+    # main.py:228-230 slices all three by --dataset-start
+    sub = images[2:]
+    assert len(sub) == len(images) - 2 and sub.names == images.names[2:]
+
+
+def test_align_data_with_an_image_array_vs_reference(golden):
+    """align_data's image branch on an (n, h, w, 3) array shorter than the
+    timestamps (it loops over images.shape[0]), returning the array itself."""
+    import src.dataloader as dl
+    d = golden("dataloader_ref.npz")
+    e = np.load(os.path.join(GOLDEN, "lcm_expected.npz"))
+    ref = _ref_clouds(d)
+    ts = d["img_timestamps"]
+    images = np.zeros((4, 2, 3, 3), dtype=np.uint8)
+    o, c, im = dl.align_data(e["odo"].astype(float), e["odo_t"].astype(float), ref, e["lid_t"].astype(float),
+                             images, ts)
+    assert im is images and np.array_equal(o, d["img4_odometry"])
+    assert all(p is ref[k] for p, k in zip(c, d["img4_cloud_index"]))
+
+
+def test_image_sequence_is_lazy(tmp_path):
+    """Frames: shape from the PNG header without decoding; reading pixels
+    needs OpenCV, and says so when it is absent."""
+    import src.dataloader as dl
+    (tmp_path / "raw_images").mkdir()
+    from PIL import Image
+    Image.new("RGB", (7, 5)).save(tmp_path / "raw_images" / "image0.png")
+    Image.new("RGB", (7, 5)).save(tmp_path / "raw_images" / "image1.png")
+    (tmp_path / "image_timestamps.txt").write_text("0, 1.5\n1, 2.0\n")
+    ims, ts = dl.get_images(str(tmp_path), np.inf, -1)
+    assert ims.shape == (2, 5, 7, 3) and ims.ndim == 4 and ts.tolist() == [1.5e6, 2.0e6]
+    assert ims[1:].shape == (1, 5, 7, 3) and ims[[1, 0]].names == ["1", "0"]
+    try:
+        import cv2  # noqa: F401
+    except ImportError:
+        with pytest.raises(ImportError, match="OpenCV"):
+            ims[0]
 
 
 def test_bad_log_raises(tmp_path):

@@ -429,11 +429,17 @@ def main():
     evals = float(np.sum(res.iters * n1 * n2))
     t = torch.tensor([dt, evals, float(B), float(res.iters.sum())], dtype=torch.float64,
                      device=ss.device if args.dist_backend == "nccl" else "cpu")
+    per_rank = None
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         t[0] = tmax[0]
+        # every rank's shard and its kernel time (the slowest shard bounds the job)
+        mine = torch.tensor([kern_ms, float(B), dt / args.steps * 1e3], dtype=torch.float64, device=t.device)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[float(x) for x in r.cpu()] for r in allr]
     dt_max, evals_all, pairs_all, iters_all = [float(x) for x in t.cpu()]
     if rank != 0:
         if world > 1:
@@ -542,6 +548,14 @@ def main():
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 6), "algorithmic_bytes_per_launch": alg_bytes},
         },
     }
+    if per_rank is not None:
+        out["per_rank"] = {"kernel_ms": [round(r[0], 4) for r in per_rank],
+                           "pairs": [int(r[1]) for r in per_rank],
+                           "wall_ms_per_step": [round(r[2], 4) for r in per_rank],
+                           "max_shard_pairs": int(max(r[1] for r in per_rank)),
+                           "slowest_rank": int(np.argmax([r[0] for r in per_rank])),
+                           "note": "kernel_ms: HIP events around batch.launch() on each rank's stream; "
+                                   "wall: the rank's timed loop incl. the all-gather"}
     if world == 1 and not args.no_cpu_baseline:
         try:
             workers = args.cpu_workers or default_cpu_workers()

@@ -51,7 +51,8 @@ def numpy_build():
     build whose matmul rounding grid_ref.npz pins (tests/test_occupancy.py)."""
     from threadpoolctl import threadpool_info
     blas = sorted(f"{i.get('internal_api')}-{i.get('version')}-{i.get('architecture')}"
-                  for i in threadpool_info() if i.get("user_api") == "blas")
+                  for i in threadpool_info()
+                  if i.get("user_api") == "blas" and "numpy" in str(i.get("filepath", "")))
     return f"numpy {np.__version__}; blas {','.join(blas)}"
 
 

@@ -59,7 +59,8 @@ def _numpy_build():
     """This host's NumPy and BLAS build, as tests/golden/gen_grid.py records it."""
     from threadpoolctl import threadpool_info
     blas = sorted(f"{i.get('internal_api')}-{i.get('version')}-{i.get('architecture')}"
-                  for i in threadpool_info() if i.get("user_api") == "blas")
+                  for i in threadpool_info()
+                  if i.get("user_api") == "blas" and "numpy" in str(i.get("filepath", "")))
     return f"numpy {np.__version__}; blas {','.join(blas)}"
 
 

@@ -2455,6 +2455,9 @@ static thread_local int g_bulk_gang_below = 0;
 static thread_local int g_bulk_gang_parts = 2;
 // carry the paused pairs' search state from phase 1 to phase 2 (warm resume)
 static thread_local int g_sched_warm = 0;
+// batches of <= kSortOneMax pairs sort on one workgroup (diagnostics: 0 = the
+// three-kernel sort at every size)
+static thread_local int g_sched_sort_one = 1;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
@@ -2684,6 +2687,83 @@ __global__ __launch_bounds__(kSortBlock) void sched_scatter_kernel(const int32_t
     }
 }
 
+// The same stable order as count + scan + scatter for a batch of at most
+// kSortOneMax pairs, in ONE workgroup (one launch instead of three, the phase
+// boundary of a strong-scaling shard is a chain of launches): an LDS histogram
+// of every pair's bucket, an exclusive scan of the bucket totals, then the
+// pairs in chunks of kSortBlock in index order, each placed at its bucket's
+// running offset plus its rank among the chunk's earlier pairs of that bucket.
+// The workgroup also zeroes `nz` words at `zero` (the phase-2 exchange slots:
+// no separate memset on the boundary).
+constexpr int kSortOneMax = 4096;
+__global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_t* __restrict__ iters,
+                                                                    const float* __restrict__ key, int32_t B,
+                                                                    float thresh, int32_t* __restrict__ order,
+                                                                    uint64_t* __restrict__ zero, int64_t nz) {
+    constexpr int WAVES = kSortBlock / 64;
+    constexpr int PER = kSortOneMax / kSortBlock;
+    __shared__ int base[kNB];
+    __shared__ int cnt[WAVES * kNB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int64_t e = tid; e < nz; e += kSortBlock) zero[e] = 0;
+    for (int i = tid; i < kNB; i += kSortBlock) base[i] = 0;
+    __syncthreads();
+    int q[PER];
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+        const int b = c * kSortBlock + tid;
+        q[c] = b < B ? sched_bucket(iters, key, b, thresh) : -1;
+        if (q[c] >= 0) atomicAdd(&base[q[c]], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of the kNB totals by wave 0 (chunks of 64 + a running carry)
+        int carry = 0;
+        for (int c0 = 0; c0 < kNB; c0 += 64) {
+            const int i = c0 + lane;
+            const int v = i < kNB ? base[i] : 0;
+            int x = v;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            if (i < kNB) base[i] = carry + x - v;
+            carry += __shfl(x, 63, 64);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+        if (c * kSortBlock >= B) break;   // uniform
+        for (int i = tid; i < WAVES * kNB; i += kSortBlock) cnt[i] = 0;
+        __syncthreads();
+        const bool valid = q[c] >= 0;
+        int rank = 0;
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const int u = __shfl(q[c], static_cast<int>(__builtin_ctzll(todo)), 64);
+            const uint64_t m = __ballot(q[c] == u);
+            if (q[c] == u) rank = __popcll(m & ((1ull << lane) - 1));
+            if (lane == 0) cnt[wave * kNB + u] = __popcll(m);
+            todo &= ~m;
+        }
+        __syncthreads();
+        if (valid) {
+            int pos = base[q[c]] + rank;
+            for (int w = 0; w < wave; ++w) pos += cnt[w * kNB + q[c]];
+            order[pos] = c * kSortBlock + tid;
+        }
+        __syncthreads();
+        // the chunk's totals advance the running offsets (one thread per bucket)
+        for (int i = tid; i < kNB; i += kSortBlock) {
+            int t = 0;
+            for (int w = 0; w < WAVES; ++w) t += cnt[w * kNB + i];
+            base[i] += t;
+        }
+        __syncthreads();
+    }
+}
+
 static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t max_n2, void* stream) {
     const int probe = g_sched_probe >= 0 ? g_sched_probe : sched_probe_for(B);
     if (probe <= 0 || B < g_sched_min_pairs || args.max_iters + 2 <= probe)
@@ -2755,14 +2835,20 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     }
     if (rc == 0) {
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
-        if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
         // phase 2 gives pairs new slots: clear phase 1's granules (a pair restarted
         // from iteration 0 would otherwise meet another pair's old tags)
         if (bg) (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
-        hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr, hist,
-                           bucket);
-        hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
-        hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, s, bucket, B, hist, order);
+        if (B <= kSortOneMax && g_sched_sort_one) {
+            // one launch on the phase boundary: the sort, and the exchange slots zeroed beside it
+            hipLaunchKernelGGL(sched_sort_one_kernel, dim3(1), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
+                               order, gang_slots, static_cast<int64_t>(G + Wd > 0 ? gang_slot_bytes / sizeof(uint64_t) : 0));
+        } else {
+            if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
+            hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
+                               hist, bucket);
+            hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
+            hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, s, bucket, B, hist, order);
+        }
         rc = check_launch("icp scheduler kernels");
     }
     if (rc == 0) {   // phase 2: the unfinished pairs, slowest-converging first
@@ -2910,6 +2996,12 @@ int slam_icp_set_schedule_warm(int on) {
     g_sched_warm = on ? 1 : 0;
     return ok();
 }
+// Diagnostics: the phase boundary's sort of batches <= 4,096 pairs on one
+// workgroup (1, default) or as the three-kernel sort (0).  Same order.
+int slam_icp_set_sched_sort_one(int on) {
+    g_sched_sort_one = on ? 1 : 0;
+    return ok();
+}
 int slam_icp_gang_timeouts(void) {
     int v = 0;
     const int zero = 0;
@@ -2934,6 +3026,11 @@ int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float
     if (B <= 0) return ok();
     if (!iters || !key || !order) return fail(SLAM_EINVAL, "null array argument");
     hipStream_t s = as_stream(stream);
+    if (B <= kSortOneMax) {   // the one-workgroup sort launch_batch uses at this size
+        hipLaunchKernelGGL(sched_sort_one_kernel, dim3(1), dim3(kSortBlock), 0, s, iters, key, B, thresh, order,
+                           static_cast<uint64_t*>(nullptr), static_cast<int64_t>(0));
+        return check_launch("sched sort kernel");
+    }
     const int nblk = (B + kSortBlock - 1) / kSortBlock;
     void* ws = nullptr;
     const size_t bytes = (static_cast<size_t>(nblk) * kNB + static_cast<size_t>(B)) * sizeof(int32_t);

@@ -281,6 +281,10 @@ int slam_icp_set_gang_wait(uint32_t ticks);
  * bucket sort (device arrays; order[] receives B pair indices). */
 int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float thresh, int32_t* order,
                         void* stream);
+/* Diagnostics: batches of <= 4,096 pairs sort at the phase boundary on one
+ * workgroup (1, default; slam_icp_sched_sort uses it at those sizes too) or
+ * with the three-kernel sort (0).  The order is the same. */
+int slam_icp_set_sched_sort_one(int on);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver (per host thread): 0 auto (block cyclic reduction when the
  * band allows it), 1 band Cholesky, 2 block cyclic reduction (falls back to 1

@@ -510,20 +510,28 @@ def test_gang_timeouts_are_repaired(k):
     assert lib.slam_icp_gang_timeouts() == 0
 
 
-def test_scheduler_order_is_a_stable_sort():
+@pytest.mark.parametrize("B", [5000, 4096, 1250, 37])
+def test_scheduler_order_is_a_stable_sort(B):
     """Phase 2's visiting order is the scheduler's stable bucket sort: the same
     permutation every run, unfinished pairs by bucket of log2 |dE| (largest
     |dE| first, 8 buckets per octave), pair index ascending inside a bucket,
-    finished pairs last in index order."""
+    finished and out-of-bounds pairs last in index order, pairs that never
+    started (out_iters 0: a timed-out phase-1 gang; key never written) first.
+    B > 4,096: the three-kernel sort; B <= 4,096: the one-workgroup sort of
+    the strong-scaling shards."""
     import ctypes
     import torch
     from slamhip import _abi
     lib = _abi.lib()
     rng = np.random.default_rng(4)
-    B, thresh = 5000, 1e-4
+    thresh = 1e-4
     kq = rng.integers(-40, 120, B)                             # bucket 128 - 8 log2(key / thresh) = 127 - kq
     key = (thresh * np.exp2((kq + 0.5) / 8.0)).astype(np.float32)   # mid-bucket: no rounding ambiguity
-    iters = np.where(rng.random(B) < 0.2, 7, -4).astype(np.int32)  # 20 % finished in phase 1
+    u = rng.random(B)
+    iters = np.where(u < 0.2, 7, -4).astype(np.int32)             # 20 % finished in phase 1
+    iters[(u >= 0.2) & (u < 0.23)] = 0                            # never started: bucket 0
+    iters[(u >= 0.23) & (u < 0.25)] = np.iinfo(np.int32).min      # out of bounds: last
+    key[iters == 0] = np.float32(np.nan)                          # unwritten key: never read
     dev = torch.device("cuda", 0)
     d_it = torch.tensor(iters, device=dev)
     d_key = torch.tensor(key, device=dev)
@@ -535,7 +543,8 @@ def test_scheduler_order_is_a_stable_sort():
         torch.cuda.synchronize()
         outs.append(d_ord.cpu().numpy())
     assert all(np.array_equal(o, outs[0]) for o in outs[1:])
-    bucket = np.where(iters > 0, 256, np.clip(127 - kq, 0, 255))
+    bucket = np.where((iters > 0) | (iters == np.iinfo(np.int32).min), 256,
+                      np.where(iters == 0, 0, np.clip(127 - kq, 0, 255)))
     want = np.lexsort((np.arange(B), bucket))
     assert np.array_equal(outs[0], want)
 

@@ -1,7 +1,9 @@
 """Scheduler settings vs batch size, in one process: rank 0's shard of the C3
 stream (first P pairs) for P in 1250 / 2500 / 5000 / 10000, timed with HIP
 events (median of 7 launches) under each setting
-"heads,gangs,parts,wide,share,bulk_below,bulk_parts,probe[,warm]".  GPU only.
+"heads,gangs,parts,wide,share,bulk_below,bulk_parts,probe[,warm[,sort_one]]"
+(probe -1: automatic; warm default 0 and sort_one 1, the product defaults).  SWEEP_SIZES=1250,2500 picks
+the batch sizes.  GPU only.
 
     python tools/sched_sweep.py [setting ...]
 """
@@ -35,7 +37,7 @@ def main():
     from slamhip import icp as k
     lib = _abi.lib()
     settings = sys.argv[1:] or DEFAULT
-    sizes = [1250, 2500, 5000, 10000]
+    sizes = [int(x) for x in os.environ.get("SWEEP_SIZES", "1250,2500,5000,10000").split(",")]
     seq = synthetic.make_sequence(10001, seed=2025)
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, 10001)])
     ss = k.ScanSet(seq.scans)
@@ -46,12 +48,13 @@ def main():
         for st in settings:
             v = [int(x) for x in st.split(",")]
             h, g, gp, w, ws, bb, bp, pr = v[:8]
-            assert lib.slam_icp_set_schedule_warm(v[8] if len(v) > 8 else 1) == 0
+            assert lib.slam_icp_set_schedule_warm(v[8] if len(v) > 8 else 0) == 0
             assert lib.slam_icp_set_schedule_heads(h) == 0
             assert lib.slam_icp_set_schedule_gangs(g, gp) == 0
             assert lib.slam_icp_set_schedule_wide(w, ws) == 0
             assert lib.slam_icp_set_bulk_gangs(bb, bp) == 0
             assert lib.slam_icp_set_schedule(pr, 1024) == 0
+            assert lib.slam_icp_set_sched_sort_one(v[9] if len(v) > 9 else 1) == 0
             out = []
             for P in sizes:
                 b = batches[P]
@@ -77,7 +80,8 @@ def main():
         lib.slam_icp_set_schedule_wide(0, 1)
         lib.slam_icp_set_bulk_gangs(0, 2)
         lib.slam_icp_set_schedule(-1, 1024)
-        lib.slam_icp_set_schedule_warm(1)
+        lib.slam_icp_set_schedule_warm(0)
+        lib.slam_icp_set_sched_sort_one(1)
 
 
 if __name__ == "__main__":

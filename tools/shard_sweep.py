@@ -1,0 +1,90 @@
+"""Strong-scaling projection on ONE GPU, done the way bench.py shards: every
+rank's shard of the ONE 10k C3 stream (slamhip.dist.shard_range over N ranks,
+N = 2, 4, 8) timed on its own (HIP events, median of 5 launches), under each
+scheduler setting "heads,gangs,parts,wide,share[,probe[,sort_one]]".  The
+projected N-GPU time is the slowest shard (bench.py takes the max over ranks).
+(bench.py --pairs P builds ANOTHER stream of P pairs: synthetic.make_sequence
+draws its noise after the whole trajectory, so a shorter stream is not a
+prefix of the 10k one.)  GPU only.
+
+    python tools/shard_sweep.py [setting ...]
+"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "icp-slam-with-loop-closure_amd"))
+
+
+def main():
+    import torch
+    torch.cuda.set_device(0)
+    from slamhip import _abi, se2, synthetic
+    from slamhip import dist as sd
+    from slamhip import icp as k
+    lib = _abi.lib()
+    settings = sys.argv[1:] or ["64,24,4,0,1"]
+    total = int(os.environ.get("SHARD_TOTAL", "10000"))
+    seq = synthetic.make_sequence(total + 1, seed=2025)
+    inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, total + 1)])
+    ss = k.ScanSet(seq.scans)
+    ranks = [int(x) for x in os.environ.get("SHARD_N", "2,4,8").split(",")]
+    batches = {}
+    for n in [1] + ranks:
+        for r in range(n):
+            lo, hi, _ = sd.shard_range(total, n, r)
+            batches[(n, r)] = k.IcpBatch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi],
+                                         epsilon=0.05, max_iters=100)
+    ref = {}
+
+    def timed(b, reps=5):
+        b.launch()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            b.launch()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return float(np.median(ts))
+    try:
+        for st in settings:
+            v = [int(x) for x in st.split(",")]
+            h, g, gp, w, ws = v[:5]
+            assert lib.slam_icp_set_schedule_heads(h) == 0
+            assert lib.slam_icp_set_schedule_gangs(g, gp) == 0
+            assert lib.slam_icp_set_schedule_wide(w, ws) == 0
+            assert lib.slam_icp_set_schedule(v[5] if len(v) > 5 else -1, 1024) == 0
+            assert lib.slam_icp_set_sched_sort_one(v[6] if len(v) > 6 else 1) == 0
+            line = []
+            t1 = None
+            for n in [1] + ranks:
+                ts = []
+                for r in range(n):
+                    b = batches[(n, r)]
+                    ts.append(timed(b, 3 if n == 1 else 5))
+                    res = b.result()
+                    key = (n, r)
+                    if key not in ref:
+                        ref[key] = res
+                    elif not (np.array_equal(res.tf, ref[key].tf) and np.array_equal(res.iters, ref[key].iters)):
+                        line.append(f"MISMATCH n{n}r{r}")
+                mx = max(ts)
+                if n == 1:
+                    t1 = mx
+                line.append(f"N{n}: max {mx:.3f} ({t1 / mx:.2f}x) shards " + " ".join(f"{t:.3f}" for t in ts))
+            print(f"h,g,k,w,s {st:16s} | " + " | ".join(line), flush=True)
+    finally:
+        lib.slam_icp_set_schedule_heads(64)
+        lib.slam_icp_set_schedule_gangs(24, 4)
+        lib.slam_icp_set_schedule_wide(0, 1)
+        lib.slam_icp_set_schedule(-1, 1024)
+        lib.slam_icp_set_sched_sort_one(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1009,7 +1009,7 @@ bool bcr_gj_default() {
 // D, E0 and bz (gn_assemble_kernel with a block layout): no load launch.
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
               double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
-              const double* BR, int32_t nbd, int32_t nvt, bool preloaded) {
+              const double* BR, int32_t nbd, int32_t nvt, bool preloaded, const BcrSchur* sc) {
     const int nb = (nv + Wb - 1) / Wb;
     const int64_t B2 = bcr_blk(Wb);
     if (bcr_gj_default() || mc > 1 || preloaded) {
@@ -1018,9 +1018,9 @@ int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_
         if (!preloaded)
             hipLaunchKernelGGL(bcr_load_kernel, dim3(static_cast<unsigned>((tot + 255) / 256)), dim3(256), 0, st, Hb,
                                rhs, nv, W, Wb, nb, g.D, g.E0, g.bz, mc, BR, nbd, nvt);
-        int rc = bcr_gj_levels(g, nv, Wb, mc, status, st);   // levels + block 0
+        int rc = bcr_gj_levels(g, nv, Wb, mc, status, st, sc);   // levels + block 0 (+ the Schur border)
         if (rc != 0) return rc;
-        rc = bcr_gj_back(g, nv, Wb, mc, st);
+        rc = bcr_gj_back(g, nv, Wb, mc, st, sc);
         *dx_out = g.x;
         return rc;
     }

@@ -68,6 +68,8 @@ struct Lds {
     static constexpr size_t bytes = doubles * sizeof(double);
     // bordered solves (several right-hand-side columns): + one RHS column tile
     static constexpr size_t bytes_multi = bytes + static_cast<size_t>(WB) * LDC * sizeof(double);
+    // Schur-accumulating bordered solves: + the whole RHS block [WB][mc + 1], mc <= 32
+    static constexpr size_t bytes_schur = bytes_multi + static_cast<size_t>(WB) * 33 * sizeof(double);
 };
 
 // D_i (WB x WB, global, row-major) -> A (LDS): every load in flight at once.
@@ -264,7 +266,8 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
                                                       double* __restrict__ SN, double* __restrict__ bz,
                                                       double* __restrict__ SPb, double* __restrict__ SNb, int32_t nb,
                                                       int32_t s, int32_t cpw, int32_t n_odd, int32_t mc,
-                                                      int32_t* __restrict__ status) {
+                                                      int32_t* __restrict__ status, double* __restrict__ bzo,
+                                                      const int32_t* __restrict__ pslot, double* __restrict__ Pw) {
     using L = Lds<T>;
     constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, K4 = WB / 4;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -272,6 +275,7 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
     double* C = A + WB * LDA;
     double* vz = C + WB * LDC;   // [2][WB]: b_i, z_i
     double* Rt = vz + 2 * WB;    // mc > 1: the workgroup's RHS column tile [WB][LDC]
+    double* Ry = Rt + WB * LDC;  // Schur solves: the whole reduced RHS block Y_i [WB][mc + 1]
     const int ng = (T + cpw - 1) / cpw;
     // mc > 1 (bordered solve): the right-hand side is a
     // WB x mc block per block row (row stride mc) in mc / 16 column tiles, one
@@ -356,6 +360,8 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
             A[(e / WB) * LDA + e % WB] = g[qq];
         }
     }
+    // Schur solve: this block's P_i slot (every RHS tile workgroup needs all of Y_i)
+    const int pk = (rwg && pslot) ? pslot[i] : -1;
     if (rwg) {
         // RHS tile with the previous level's updates folded in (as D_i)
         const int64_t RB = static_cast<int64_t>(WB) * mc;
@@ -367,6 +373,17 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
                 if (i + sp < nb) v -= SPb[(i + sp) * RB + r * mc + c];
             }
             Rt[r * LDC + (e & 15)] = v;
+        }
+        if (pk >= 0) {   // the whole Y_i, the same subtraction order
+            for (int e = tid; e < WB * mc; e += kThreads) {
+                const int r = e / mc, c = e - r * mc;
+                double v = bz[i * RB + e];
+                if (sp > 0) {
+                    v -= SNb[(i - sp) * RB + e];
+                    if (i + sp < nb) v -= SPb[(i + sp) * RB + e];
+                }
+                Ry[r * (mc + 1) + c] = v;
+            }
         }
     }
     if (zwg && tid < WB) {
@@ -389,7 +406,7 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
         // RHS tile: z_i's columns 16 tj.. (bz, row stride mc), then E_p^T z (SPb)
         // and E_i z (SNb) as the X side's Sp and E' (sign +)
         const int64_t RB = static_cast<int64_t>(WB) * mc;
-        double* Out1 = rwg ? bz + i * RB + 16 * tj : (xside ? Xs : Ys) + i * B2 + 16 * tj;
+        double* Out1 = rwg ? (bzo ? bzo : bz) + i * RB + 16 * tj : (xside ? Xs : Ys) + i * B2 + 16 * tj;
         const int ld1 = rwg ? mc : WB;
         {
             constexpr int N1 = (T + 3) / 4;
@@ -456,6 +473,25 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
         }
         __syncthreads();   // C is rewritten by the next column tile
         GJ_STAMP(6);
+    }
+    if (pk >= 0) {
+        // P_i[:, tile] = Y_i^T Z_i[:, tile]: Y_i in Ry, this tile of Z_i = G_i Y_i
+        // still in C (rwg: one column tile, its loop body ran once)
+        const int ti = wave;
+        if (ti < mc / 16) {
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+            double af[K4], bf[K4];
+#pragma unroll
+            for (int k4 = 0; k4 < K4; ++k4) {
+                af[k4] = Ry[(4 * k4 + lk) * (mc + 1) + 16 * ti + lr];
+                bf[k4] = C[(4 * k4 + lk) * LDC + lr];
+            }
+#pragma unroll
+            for (int k4 = 0; k4 < K4; ++k4) acc = mma(af[k4], bf[k4], acc);
+            double* P = Pw + static_cast<int64_t>(pk) * mc * mc;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) P[(16 * ti + lk + 4 * g) * mc + 16 * tj0 + lr] = acc[g];
+        }
     }
     if (zwg) {
         // three mat-vecs, each over the whole workgroup: rows r = lane, lane + 64
@@ -579,6 +615,125 @@ __global__ __launch_bounds__(kThreads) void top_kernel(const double* __restrict_
     if (tid < WB) x[tid] = ((red[tid] + red[WB + tid]) + red[2 * WB + tid]) + red[3 * WB + tid];
 }
 
+// Block 0 of a Schur-accumulating bordered solve (gn_bcr.hpp BcrSchur), one
+// workgroup: D_0 and its reduced RHS block R_0 = [b_0 | y_0] (the last level's
+// Sp folded in), X_0 = G_0 R_0, then the border: S = C - sum_k P_k[B, B] -
+// R_0[:, B]^T X_0[:, B] and s = r_b - (the same with column 0), the slots in
+// slot order (deterministic), S padded to 32 x 32 with the identity and
+// inverted by gj_invert<2>, x_b = S^-1 s; and x_0 = X_0[:, 0] - X_0[:, B] x_b.
+template <int T>
+__global__ __launch_bounds__(kThreads) void top_schur_kernel(const double* __restrict__ D,
+                                                            const double* __restrict__ SP,
+                                                            const double* __restrict__ bz,
+                                                            const double* __restrict__ SPb, double* __restrict__ x,
+                                                            int32_t sl, int32_t mc, BcrSchur sc,
+                                                            int32_t* __restrict__ status, int32_t* ready, int32_t nb) {
+    using L = Lds<T>;
+    constexpr int WB = L::WB, LDA = L::LDA, LDC = 17, PER = T * T;
+    constexpr int WC = WB > 32 ? WB : 32;   // C scratch rows (the 32 x 32 border inverse too)
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* A = lds;                  // [WB][LDA]: D_0, then G_0
+    double* C = A + WB * LDA;         // [WC][17]
+    double* R = C + WC * LDC;         // [WB][mc + 1]: R_0
+    double* X0 = R + WB * (mc + 1);   // [WB][mc + 1]: X_0 = G_0 R_0
+    double* Sm = X0 + WB * (mc + 1);  // [32][33]: S, then S^-1
+    double* sv = Sm + 32 * 33;        // [32]: s
+    double* xbs = sv + 32;            // [32]: x_b
+    const int tid = threadIdx.x;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
+    // the fused back-substitution's ready flags: cleared here (this launch
+    // ends before it starts), block 0's set at the end
+    for (int j = tid + 1; j < nb; j += kThreads) ready[j] = 0;
+    {
+        double g[PER], a1[PER];
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) {
+            g[qq] = D[tid + kThreads * qq];
+            a1[qq] = sl > 0 ? SP[sl * B2 + tid + kThreads * qq] : 0.0;
+        }
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) {
+            const int e = tid + kThreads * qq;
+            A[(e / WB) * LDA + e % WB] = sl > 0 ? g[qq] - a1[qq] : g[qq];
+        }
+    }
+    for (int e = tid; e < WB * mc; e += kThreads) {
+        const double v = bz[e];
+        R[(e / mc) * (mc + 1) + e % mc] = sl > 0 ? v - SPb[sl * RB + e] : v;
+    }
+    __syncthreads();
+    if (gj_invert<T>(A, C) && tid == 0) *status = 1;   // ends with a barrier
+    for (int e = tid; e < WB * mc; e += kThreads) {
+        const int r = e / mc, c = e % mc;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < WB; ++k) acc = fma(A[r * LDA + k], R[k * (mc + 1) + c], acc);
+        X0[r * (mc + 1) + c] = acc;
+    }
+    __syncthreads();
+    // [S | s] entries e = k * (nbd + 1) + l (l = nbd: s), at most 4 per thread
+    const int nbd = sc.nbd, ncol = nbd + 1;
+    for (int e = tid; e < 32 * 32; e += kThreads) {   // identity padding
+        const int r = e >> 5, c = e & 31;
+        if (r >= nbd || c >= nbd) Sm[r * 33 + c] = r == c ? 1.0 : 0.0;
+    }
+    if (tid < 32 && tid >= nbd) sv[tid] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = tid + kThreads * q;
+        if (e < nbd * ncol) {
+            const int k = e / ncol, l = e % ncol;
+            const int pc = l < nbd ? 1 + l : 0;   // P column: B_l, or the rhs
+            const double cv = l < nbd ? (l <= k ? sc.BR[static_cast<int64_t>(k) * sc.nvt + sc.nv_band + l]
+                                                : sc.BR[static_cast<int64_t>(l) * sc.nvt + sc.nv_band + k])
+                                      : sc.rhs[sc.nv_band + k];
+            double acc = 0.0;
+            int t = 0;
+            for (; t + 4 <= sc.n_slots; t += 4) {   // four slots' loads in flight, summed in slot order
+                double pv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) pv[u] = sc.P[(static_cast<int64_t>(t + u) * mc + 1 + k) * mc + pc];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc += pv[u];
+            }
+            for (; t < sc.n_slots; ++t) acc += sc.P[(static_cast<int64_t>(t) * mc + 1 + k) * mc + pc];
+            double p0 = 0.0;   // P_0 = R_0^T X_0
+#pragma unroll 8
+            for (int r = 0; r < WB; ++r) p0 = fma(R[r * (mc + 1) + 1 + k], X0[r * (mc + 1) + pc], p0);
+            acc += p0;
+            if (l < nbd) Sm[k * 33 + l] = cv - acc;
+            else sv[k] = cv - acc;
+        }
+    }
+    __syncthreads();
+    if (gj_invert<2>(Sm, C) && tid == 0) *status = 1;   // ends with a barrier
+    if (tid < nbd) {
+        double v = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) v = fma(Sm[tid * 33 + k], sv[k], v);
+        xbs[tid] = v;
+        sc.xb[tid] = v;
+    }
+    __syncthreads();
+    if (tid < WB) {
+        double a = 0.0;
+        for (int k = 0; k < nbd; ++k) a = fma(X0[tid * (mc + 1) + 1 + k], xbs[k], a);
+        x[tid] = X0[tid * (mc + 1)] - a;
+    }
+    if (tid == 0) ready[0] = 1;
+}
+
+// Back-substitution of a Schur-accumulating bordered solve (one column):
+// x_i = (z_i[:, 0] - z_i[:, B] x_b) - X_i x_p - Y_i x_n, z_i from bzo (row
+// stride mc).  Thread (tr, tc) sums its share of the row's terms (columns
+// tc + 16 w of X / Y, z columns tc + 16 m) and the DPP row sum adds them.
+template <int T>
+__global__ __launch_bounds__(kThreads) void back_schur_kernel(const double* __restrict__ Xs,
+                                                             const double* __restrict__ Ys,
+                                                             const double* __restrict__ bzo, double* __restrict__ x,
+                                                             const double* __restrict__ xb, int32_t nbd, int32_t nb,
+                                                             int32_t s, int32_t mc);
+
 // A double moved between lanes of a 16-lane row by DPP (both halves).
 template <int CTRL>
 __device__ __forceinline__ double dpp_row(double v) {
@@ -646,6 +801,174 @@ __global__ __launch_bounds__(kThreads) void back_kernel(const double* __restrict
             x[static_cast<int64_t>(i) * WB + r] = zv[u] - v[u];
         }
     }
+}
+
+template <int T>
+__global__ __launch_bounds__(kThreads) void back_schur_kernel(const double* __restrict__ Xs,
+                                                             const double* __restrict__ Ys,
+                                                             const double* __restrict__ bzo, double* __restrict__ x,
+                                                             const double* __restrict__ xb, int32_t nbd, int32_t nb,
+                                                             int32_t s, int32_t mc) {
+    constexpr int WB = 16 * T;
+    const int tid = threadIdx.x;
+    const int i = s + 2 * s * blockIdx.x;
+    const int p = i - s, n = i + s;
+    const bool hn = n < nb;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
+    const int tr = tid >> 4, tc = tid & 15;
+    const double* X = Xs + i * B2;
+    const double* Y = Ys + i * B2;
+    const int nzc = mc / 16;   // z columns per thread: tc + 16 m (mc <= 32)
+    double xv[T][T], yv[T][T], vp[T], vn[T], zv[T][2], cf[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {   // coefficient of z column c: 1 (the rhs), -x_b[c - 1], 0 past the border
+        const int c = tc + 16 * m;
+        cf[m] = m < nzc ? (c == 0 ? 1.0 : (c <= nbd ? -xb[c - 1] : 0.0)) : 0.0;
+    }
+#pragma unroll
+    for (int w = 0; w < T; ++w) {
+        vp[w] = x[static_cast<int64_t>(p) * WB + tc + 16 * w];
+        vn[w] = hn ? x[static_cast<int64_t>(n) * WB + tc + 16 * w] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            xv[u][w] = X[(tr + 16 * u) * WB + tc + 16 * w];
+            yv[u][w] = hn ? Y[(tr + 16 * u) * WB + tc + 16 * w] : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+            zv[u][m] = m < nzc ? bzo[i * RB + static_cast<int64_t>(tr + 16 * u) * mc + tc + 16 * m] : 0.0;
+    }
+    double v[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int w = 0; w < T; ++w) {
+            a0 = fma(xv[u][w], vp[w], a0);
+            a1 = fma(yv[u][w], vn[w], a1);
+        }
+        v[u] = (a0 + a1) - fma(cf[1], zv[u][1], cf[0] * zv[u][0]);   // -(this thread's share of x)
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        v[u] += dpp_row<0xB1>(v[u]);
+        v[u] += dpp_row<0x4E>(v[u]);
+        v[u] += dpp_row<0x124>(v[u]);
+        v[u] += dpp_row<0x128>(v[u]);
+    }
+    if (tc == 0) {
+#pragma unroll
+        for (int u = 0; u < T; ++u) x[static_cast<int64_t>(i) * WB + tr + 16 * u] = -v[u];
+    }
+}
+
+// Every back-substitution level of a Schur-accumulating bordered solve in ONE
+// launch (a level is a few microseconds of load latency, a kernel boundary
+// another ~1.6 us, profiles/r05_launch_ubench.txt) — measured SLOWER (the
+// flags' cross-XCD release / acquire cost more than the launches), kept
+// selectable for A/B (SLAMHIP_GN_FUSED_BACK=1): workgroup w takes the w-th
+// odd block in coarsest-level-first order, waits until the x of its two
+// neighbours is published (ready[] flags: thread 0 polls with agent-scope
+// acquire loads, then a barrier), solves as back_schur_kernel and publishes
+// its own x (barrier, then an agent-scope release store).  Producers always
+// have lower workgroup indices than their consumers, and workgroups are
+// dispatched in index order, so the lowest unfinished one can always run.
+// top_schur_kernel zeroed the flags and set block 0's.  A wait longer than
+// `wait` s_memrealtime ticks sets *status = 2 and goes on (a wrong result that
+// the caller reports, never a hang).
+template <int T>
+__global__ __launch_bounds__(kThreads) void back_schur_fused_kernel(const double* __restrict__ Xs,
+                                                                   const double* __restrict__ Ys,
+                                                                   const double* __restrict__ bzo,
+                                                                   double* x,
+                                                                   const double* __restrict__ xb, int32_t nbd,
+                                                                   int32_t nb, int32_t mc, int32_t* ready,
+                                                                   uint32_t wait, int32_t* __restrict__ status) {
+    constexpr int WB = 16 * T;
+    const int tid = threadIdx.x;
+    int w = static_cast<int>(blockIdx.x);
+    int s = 1;
+    while (2 * s < nb) s *= 2;   // the top level
+    for (;;) {
+        const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
+        if (w < n_odd || s == 1) break;
+        w -= n_odd;
+        s /= 2;
+    }
+    const int i = s + 2 * s * w;
+    if (i >= nb) return;   // (uniform) past the last odd block
+    const int p = i - s, n = i + s;
+    const bool hn = n < nb;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
+    const int tr = tid >> 4, tc = tid & 15;
+    const double* X = Xs + i * B2;
+    const double* Y = Ys + i * B2;
+    const int nzc = mc / 16;
+    // this block's own operands (written by earlier launches) in flight while
+    // thread 0 waits for the neighbours
+    double xv[T][T], yv[T][T], vp[T], vn[T], zv[T][2], cf[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int c = tc + 16 * m;
+        cf[m] = m < nzc ? (c == 0 ? 1.0 : (c <= nbd ? -xb[c - 1] : 0.0)) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+#pragma unroll
+        for (int ww = 0; ww < T; ++ww) {
+            xv[u][ww] = X[(tr + 16 * u) * WB + tc + 16 * ww];
+            yv[u][ww] = hn ? Y[(tr + 16 * u) * WB + tc + 16 * ww] : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+            zv[u][m] = m < nzc ? bzo[i * RB + static_cast<int64_t>(tr + 16 * u) * mc + tc + 16 * m] : 0.0;
+    }
+    if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(ready + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 ||
+               (hn && __hip_atomic_load(ready + n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > wait) {
+                atomicOr(status, 2);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ww = 0; ww < T; ++ww) {   // the neighbours' x: after the acquire
+        vp[ww] = x[static_cast<int64_t>(p) * WB + tc + 16 * ww];
+        vn[ww] = hn ? x[static_cast<int64_t>(n) * WB + tc + 16 * ww] : 0.0;
+    }
+    double v[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < T; ++ww) {
+            a0 = fma(xv[u][ww], vp[ww], a0);
+            a1 = fma(yv[u][ww], vn[ww], a1);
+        }
+        v[u] = (a0 + a1) - fma(cf[1], zv[u][1], cf[0] * zv[u][0]);
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        v[u] += dpp_row<0xB1>(v[u]);
+        v[u] += dpp_row<0x4E>(v[u]);
+        v[u] += dpp_row<0x124>(v[u]);
+        v[u] += dpp_row<0x128>(v[u]);
+    }
+    if (tc == 0) {
+#pragma unroll
+        for (int u = 0; u < T; ++u) x[static_cast<int64_t>(i) * WB + tr + 16 * u] = -v[u];
+    }
+    // every wave's x stores made visible at agent scope, then one flag
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(ready + i, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Bordered solves: x_i = z_i - X_i x_p - Y_i x_n for WB x mc blocks (row
@@ -816,21 +1139,26 @@ BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc) {
     b.SPb = b.bz + nb * RB;
     b.SNb = b.SPb + nb * RB;
     b.x = b.SNb + nb * RB;
+    b.bzo = b.x + nb * RB;
+    b.ready = reinterpret_cast<int32_t*>(b.bzo + nb * RB);
     return b;
 }
 
 int64_t bcr_gj_work_size(int32_t nv, int32_t Wb, int32_t mc) {
     const int64_t nb = (nv + Wb - 1) / Wb;
-    return 7 * nb * Wb * Wb + 4 * nb * Wb * static_cast<int64_t>(mc);
+    return 7 * nb * Wb * Wb + 5 * nb * Wb * static_cast<int64_t>(mc) + nb;   // + the ready flags
 }
 
 // The levels of the explicit-inverse reduction, after bcr_load_kernel filled
 // D, E0 and bz, and the block-0 solve (x_0 in b.x).
-int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_t* status, hipStream_t st) {
+int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_t* status, hipStream_t st,
+                  const BcrSchur* sc) {
     const int nb = (nv + Wb - 1) / Wb;
     const int mct = mc > 1 ? mc / 16 : 0;   // RHS column tiles (bordered solves)
+    if (sc && (mc > 32 || mc < 16)) return fail(SLAM_EINVAL, "gn: Schur border with %d RHS columns", mc);
     using OddFn = void (*)(double*, const double*, double*, double*, double*, double*, double*, double*,
-                           double*, double*, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t*);
+                           double*, double*, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t*, double*,
+                           const int32_t*, double*);
     static const OddFn odds[6] = {bcrgj::odd_kernel<1>, bcrgj::odd_kernel<2>, bcrgj::odd_kernel<3>,
                                   bcrgj::odd_kernel<4>, bcrgj::odd_kernel<5>, bcrgj::odd_kernel<6>};
     static const size_t lds1[6] = {bcrgj::Lds<1>::bytes, bcrgj::Lds<2>::bytes, bcrgj::Lds<3>::bytes,
@@ -838,12 +1166,15 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
     static const size_t ldsm[6] = {bcrgj::Lds<1>::bytes_multi, bcrgj::Lds<2>::bytes_multi,
                                    bcrgj::Lds<3>::bytes_multi, bcrgj::Lds<4>::bytes_multi,
                                    bcrgj::Lds<5>::bytes_multi, bcrgj::Lds<6>::bytes_multi};
-    const size_t* lds = mct > 0 ? ldsm : lds1;
+    static const size_t ldss[6] = {bcrgj::Lds<1>::bytes_schur, bcrgj::Lds<2>::bytes_schur,
+                                   bcrgj::Lds<3>::bytes_schur, bcrgj::Lds<4>::bytes_schur,
+                                   bcrgj::Lds<5>::bytes_schur, bcrgj::Lds<6>::bytes_schur};
+    const size_t* lds = sc ? ldss : mct > 0 ? ldsm : lds1;
     static bool attrs = false;
     if (!attrs) {   // not a stream operation: the launch sequence stays graph-capturable
         for (int t = 0; t < 6; ++t)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(odds[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      static_cast<int>(ldsm[t]));
+                                      static_cast<int>(ldss[t]));
         attrs = true;
     }
     const int T = Wb / 16;
@@ -873,7 +1204,8 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
         const int n_comb = s > 1 ? n_even : 0;
         hipLaunchKernelGGL(odds[T - 1], dim3(n_odd + n_comb, max(2 * ng + max(mct, 1), bcrgj::kCombineSplit)),
                            dim3(bcrgj::kThreads), lds[T - 1], st, b.D, Ec, En, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb,
-                           b.SNb, nb, s, cpw, n_odd, mc, status);
+                           b.SNb, nb, s, cpw, n_odd, mc, status, sc ? b.bzo : nullptr, sc ? sc->pslot : nullptr,
+                           sc ? sc->P : nullptr);
         last = s;
     }
     // block 0 (always even): the last level's Sp, then x_0
@@ -887,6 +1219,28 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(tops[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       static_cast<int>(lds1[t] + sizeof(double) * 96 * 65));
         attrs_t = true;
+    }
+    if (sc) {   // block 0 + the border's Schur complement and x_b
+        using TopSFn = void (*)(const double*, const double*, const double*, const double*, double*, int32_t, int32_t,
+                                BcrSchur, int32_t*, int32_t*, int32_t);
+        static const TopSFn topss[6] = {bcrgj::top_schur_kernel<1>, bcrgj::top_schur_kernel<2>,
+                                        bcrgj::top_schur_kernel<3>, bcrgj::top_schur_kernel<4>,
+                                        bcrgj::top_schur_kernel<5>, bcrgj::top_schur_kernel<6>};
+        auto top_s_lds = [](int wb) {
+            const int wc = wb > 32 ? wb : 32;
+            return sizeof(double) * (static_cast<size_t>(wb) * (wb + 1) + static_cast<size_t>(wc) * 17 +
+                                     2 * static_cast<size_t>(wb) * 33 + 32 * 33 + 64);
+        };
+        static bool attrs_s = false;
+        if (!attrs_s) {
+            for (int t = 0; t < 6; ++t)
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topss[t]),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(top_s_lds(16 * (t + 1))));
+            attrs_s = true;
+        }
+        hipLaunchKernelGGL(topss[T - 1], dim3(1), dim3(bcrgj::kThreads), top_s_lds(Wb), st, b.D, b.SP, b.bz, b.SPb,
+                           b.x, nb > 1 ? last : 0, mc, *sc, status, b.ready, nb);
+        return check_launch("gn bcr (explicit inverse, Schur border) kernels");
     }
     const size_t lds_top = lds1[T - 1] + (mct > 0 ? sizeof(double) * Wb * (mc + 1) : 0);
     hipLaunchKernelGGL(tops[T - 1], dim3(1), dim3(bcrgj::kThreads), lds_top, st, b.D, b.SP, b.bz, b.SPb, b.x,
@@ -904,8 +1258,40 @@ int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const
     return check_launch("gn border solve");
 }
 
-int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st) {
+int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st, const BcrSchur* sc) {
     const int nb = (nv + Wb - 1) / Wb;
+    // measured and off by default: the flag hand-offs (agent-scope release /
+    // acquire across XCDs) cost more than the launches they replace
+    // (profiles/r05_gn_ab_schur.txt: 2,926-2,949 against 5,282-5,310 it/s)
+    static const bool fused = [] {
+        const char* e = getenv("SLAMHIP_GN_FUSED_BACK");
+        return e && e[0] == '1';
+    }();
+    if (sc && fused && nb > 1) {   // every level in one launch (ready flags)
+        using BackFFn = void (*)(const double*, const double*, const double*, double*, const double*, int32_t, int32_t,
+                                 int32_t, int32_t*, uint32_t, int32_t*);
+        static const BackFFn backfs[6] = {bcrgj::back_schur_fused_kernel<1>, bcrgj::back_schur_fused_kernel<2>,
+                                          bcrgj::back_schur_fused_kernel<3>, bcrgj::back_schur_fused_kernel<4>,
+                                          bcrgj::back_schur_fused_kernel<5>, bcrgj::back_schur_fused_kernel<6>};
+        hipLaunchKernelGGL(backfs[Wb / 16 - 1], dim3(nb - 1), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bzo, b.x,
+                           sc->xb, sc->nbd, nb, mc, b.ready, static_cast<uint32_t>(10000000), sc->status);
+        return check_launch("gn bcr (explicit inverse, Schur border) fused back-substitution");
+    }
+    if (sc) {   // one column: z_i[:, 0] - z_i[:, B] x_b
+        using BackSFn = void (*)(const double*, const double*, const double*, double*, const double*, int32_t, int32_t,
+                                 int32_t, int32_t);
+        static const BackSFn backss[6] = {bcrgj::back_schur_kernel<1>, bcrgj::back_schur_kernel<2>,
+                                          bcrgj::back_schur_kernel<3>, bcrgj::back_schur_kernel<4>,
+                                          bcrgj::back_schur_kernel<5>, bcrgj::back_schur_kernel<6>};
+        int s = 1;
+        while (s < nb) s *= 2;
+        for (s /= 2; s >= 1; s /= 2) {
+            const int n_odd = (nb - s + 2 * s - 1) / (2 * s);
+            hipLaunchKernelGGL(backss[Wb / 16 - 1], dim3(n_odd), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bzo, b.x,
+                               sc->xb, sc->nbd, nb, s, mc);
+        }
+        return check_launch("gn bcr (explicit inverse, Schur border) back-substitution");
+    }
     using BackFn = void (*)(const double*, const double*, const double*, double*, int32_t, int32_t);
     static const BackFn backs[6] = {bcrgj::back_kernel<1>, bcrgj::back_kernel<2>, bcrgj::back_kernel<3>,
                                     bcrgj::back_kernel<4>, bcrgj::back_kernel<5>, bcrgj::back_kernel<6>};

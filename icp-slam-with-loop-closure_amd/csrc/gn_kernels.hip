@@ -657,6 +657,21 @@ __global__ void gn_border_update_kernel(double* __restrict__ poses, int32_t N, c
     poses[3 * n + q] = q == 2 ? wrap_pi(p0 + d) : p0 + d;
 }
 
+// The pose update of a Schur-accumulating bordered solve: dx = [x_a ; x_b]
+// (x_a the band's one-column solution, x_b the border's).
+__global__ void gn_schur_update_kernel(double* __restrict__ poses, int32_t N, const int32_t* __restrict__ node_col,
+                                       const double* __restrict__ xa, const double* __restrict__ xb, int32_t nv_band) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = t / 3, q = t - 3 * n;
+    if (n >= N) return;
+    const double p0 = poses[3 * n + q];   // in flight beside the node_col -> dx chain
+    const int c = node_col[n];
+    if (c < 0) return;
+    const int R = c + q;
+    const double d = R < nv_band ? xa[R] : xb[R - nv_band];
+    poses[3 * n + q] = q == 2 ? wrap_pi(p0 + d) : p0 + d;
+}
+
 __global__ void gn_update_kernel(double* __restrict__ poses, int32_t N, const int32_t* __restrict__ node_col,
                                  const double* __restrict__ dx) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -683,7 +698,7 @@ int bcr_block_rows(int32_t nv, int32_t W);
 int64_t bcr_work_size(int32_t nv, int32_t W, int32_t mc);
 int bcr_solve(const double* Hb, const double* rhs, int32_t nv, int32_t W, int32_t Wb, double* work,
               double** dx_out, int32_t* status, hipStream_t st, unsigned long long* stamps, int32_t mc,
-              const double* BR, int32_t nbd, int32_t nvt, bool preloaded);
+              const double* BR, int32_t nbd, int32_t nvt, bool preloaded, const BcrSchur* sc);
 bool bcr_gj_default();
 int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const int32_t* nbr_rows, int32_t n_nbr,
                      int32_t nv_band, int32_t nbd, int32_t nvt, int32_t mc, double* xb, int32_t* status,
@@ -759,7 +774,8 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
                         const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
                         const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv, int32_t W,
                         int32_t nv_band, const int32_t* nbr_rows, int32_t n_nbr, double* work, double* out_chi2,
-                        int32_t* status, void* stream) {
+                        int32_t* status, void* stream, const int32_t* pslot = nullptr, int32_t n_pslot = 0,
+                        double* pwork = nullptr) {
     if (N < 1 || E < 0 || nv < 0 || W < 2) return fail(SLAM_EINVAL, "gn: N=%d E=%d nv=%d W=%d", N, E, nv, W);
     if (!poses || !ea || !eb || !tf || !w || !node_col || !slot_rc || !slot_ptr || !work || !out_chi2 || !status)
         return fail(SLAM_EINVAL, "gn: null array argument");
@@ -815,9 +831,18 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
                            slot_ptr, slot_items, n_slots, W, Hb, rhs, nv_band, nv, BR, chi2e, n_chi2p, out_chi2, bd);
     if (Wb > 0) {   // block cyclic reduction: log2(nv / Wb) parallel levels
         double* dx = nullptr;
+        // the border's Schur complement accumulated during the elimination (needs
+        // the assembly's direct block layout; slam_gn_iteration_schur_f64)
+        const bool schur = nbd > 0 && pslot && bd.D;
+        const BcrSchur sc{pslot, pwork, n_pslot, BR, rhs, nv_band, nbd, nv, xb, status};
         const int rc = bcr_solve(Hb, rhs, nv_band, W, Wb, bwork, &dx, status, s, g_gn_stamps, mc, BR, nbd, nv,
-                                 bd.D != nullptr);
+                                 bd.D != nullptr, schur ? &sc : nullptr);
         if (rc != 0) return rc;
+        if (schur) {
+            hipLaunchKernelGGL(gn_schur_update_kernel, dim3((3 * N + 255) / 256), dim3(256), 0, s, poses, N, node_col,
+                               dx, xb, nv_band);
+            return check_launch("gn kernels");
+        }
         if (nbd > 0) {
             const int rb = bcr_border_solve(dx, BR, rhs, nbr_rows, n_nbr, nv_band, nbd, nv, mc, xb, status, s);
             if (rb != 0) return rb;
@@ -873,6 +898,19 @@ int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int
                           int32_t W, double* work, double* out_chi2, int32_t* status, void* stream) {
     return gn_iteration(poses, N, ea, eb, tf, w, E, node_col, slot_rc, slot_ptr, slot_items, n_slots, nv, W, nv,
                         nullptr, 0, work, out_chi2, status, stream);
+}
+
+int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,
+                                const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
+                                const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv,
+                                int32_t W, int32_t nv_band, const int32_t* pslot, int32_t n_pslot, double* pwork,
+                                double* work, double* out_chi2, int32_t* status, void* stream) {
+    if (nv - nv_band < 1 || !pslot || n_pslot < 0 || (n_pslot > 0 && !pwork))
+        return fail(SLAM_EINVAL, "gn schur: border %d, pslot %p, %d slots", nv - nv_band, pslot, n_pslot);
+    if (g_gn_solver == 1 || !bcr_gj_default())
+        return fail(SLAM_EINVAL, "gn schur: needs the explicit-inverse cyclic reduction (solver mode %d)", g_gn_solver);
+    return gn_iteration(poses, N, ea, eb, tf, w, E, node_col, slot_rc, slot_ptr, slot_items, n_slots, nv, W, nv_band,
+                        nullptr, 0, work, out_chi2, status, stream, pslot, n_pslot, pwork);
 }
 
 int slam_gn_iteration_bordered_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,

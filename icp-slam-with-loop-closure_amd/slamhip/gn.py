@@ -16,6 +16,7 @@ Cholesky, substitution, pose update.  Problem definition (residual, Jacobians,
 information 2 I / 5 I as src/pose_graph.py:61-73 exports them) is documented
 in csrc/gn_kernels.hip and oracle/gn_oracle.py.
 """
+import os
 import time
 
 import numpy as np
@@ -190,6 +191,9 @@ class GnPlan:
         xb = (ca >= 0) & (cb >= 0) & ((ca >= self.nv_band) != (cb >= self.nv_band))
         bn = np.where(ca[xb] < self.nv_band, ca[xb], cb[xb])
         self.nbr_rows = np.unique((bn[:, None] + np.arange(3)[None, :]).ravel()).astype(np.int32)
+        self.pslot = self.schur_blocks = None
+        if self.nv_band < self.nv:
+            self.pslot, self.schur_blocks = schur_slots(self.nbr_rows, self.nv_band, self.W)
         order = np.r_[order, border]   # every free node in column order (slots below)
 
         # diagonal slots: free node n (in RCM order), items 2e + side (a: 0, b: 1) in
@@ -243,6 +247,45 @@ def _border_allowed():
         return True
 
 
+MAX_SCHUR_SLOTS = 64   # more coupled blocks than this: the multi-column back-substitution path
+
+
+def schur_slots(nbr_rows, nv_band, W):
+    """The blocks whose reduced rows couple to the border during the block
+    cyclic reduction, symbolically: a band block
+    couples if it holds a row of nbr_rows; eliminating a coupled odd block i
+    at level s (i = s, 3s, ...) passes the coupling to its neighbours i - s and
+    i + s (the RHS update b_j -= A[j, i] z_i).  Every coupled block eliminated
+    adds Y_i^T D_i^-1 Y_i to the border's Schur complement: returns (pslot, the
+    list in elimination order) with pslot[i] = its slot, -1 elsewhere, or
+    (None, None) when the cyclic reduction does not apply or the list exceeds
+    MAX_SCHUR_SLOTS (slam_gn_iteration_bordered_f64 then)."""
+    try:
+        Wb = int(_abi.lib().slam_gn_bcr_block_rows(nv_band, W))
+    except (OSError, ImportError, AttributeError):
+        return None, None
+    if Wb <= 0 or not os.environ.get("SLAMHIP_GN_SCHUR", "1") == "1":
+        return None, None
+    nb = (nv_band + Wb - 1) // Wb
+    nz = np.zeros(nb, dtype=bool)
+    nz[np.asarray(nbr_rows, dtype=np.int64) // Wb] = True
+    blocks = []
+    s = 1
+    while s < nb:
+        for i in range(s, nb, 2 * s):
+            if nz[i]:
+                blocks.append(i)
+                nz[i - s] = True
+                if i + s < nb:
+                    nz[i + s] = True
+        s *= 2
+    if len(blocks) > MAX_SCHUR_SLOTS:
+        return None, None
+    pslot = np.full(nb, -1, dtype=np.int32)
+    pslot[blocks] = np.arange(len(blocks), dtype=np.int32)
+    return pslot, np.asarray(blocks, dtype=np.int32)
+
+
 _PLANS = {}   # structure -> GnPlan (a pipeline re-optimises the same graph structure)
 
 
@@ -286,6 +329,10 @@ class GaussNewton:
                 if p.nv_band < p.nv else _abi.lib().slam_gn_work_size(self.N, self.E, p.W))
         self.work = dv.empty((n,), np.float64, dev)
         self.status = dv.to_dev(np.zeros(1, np.int32), np.int32, dev)
+        if p.pslot is not None:   # the Schur-accumulating bordered path
+            mc = 16 * ((p.nv - p.nv_band + 16) // 16)
+            self.pslot = dv.to_dev(p.pslot, np.int32, dev)
+            self.pwork = dv.empty((max(len(p.schur_blocks), 1) * mc * mc,), np.float64, dev)
         self.chi2 = None
         self._eager_done = False
         self._graphs = {}
@@ -293,6 +340,14 @@ class GaussNewton:
     def iterate(self, chi2_out, stream=None):
         """One asynchronous GN iteration; chi2 (before the step) -> chi2_out (device)."""
         p = self.plan
+        if p.nv_band < p.nv and p.pslot is not None:
+            _abi.check(_abi.lib().slam_gn_iteration_schur_f64(
+                dv.ptr(self.poses), self.N, dv.ptr(self.ea), dv.ptr(self.eb), dv.ptr(self.tf), dv.ptr(self.w),
+                self.E, dv.ptr(self.node_col), dv.ptr(self.slot_rc), dv.ptr(self.slot_ptr), dv.ptr(self.slot_items),
+                p.n_slots, p.nv, p.W, p.nv_band, dv.ptr(self.pslot), len(p.schur_blocks), dv.ptr(self.pwork),
+                dv.ptr(self.work), dv.ptr(chi2_out), dv.ptr(self.status), dv.stream_handle(stream)),
+                "slam_gn_iteration_schur_f64")
+            return
         if p.nv_band < p.nv:
             _abi.check(_abi.lib().slam_gn_iteration_bordered_f64(
                 dv.ptr(self.poses), self.N, dv.ptr(self.ea), dv.ptr(self.eb), dv.ptr(self.tf), dv.ptr(self.w),
@@ -353,7 +408,11 @@ class GaussNewton:
                 self.iterate(chis[k:k + 1], stream)
             self._eager_done = True
         out = chis[:iterations].cpu().numpy().copy()
-        if int(self.status.cpu().numpy()[0]) != 0:
+        st = int(self.status.cpu().numpy()[0])
+        if st & 2:
+            raise _abi.SlamHipError("Gauss-Newton: the fused back-substitution timed out waiting for a block "
+                                    "(unset SLAMHIP_GN_FUSED_BACK: the per-level launches)")
+        if st != 0:
             raise _abi.SlamHipError("Gauss-Newton: H is not positive definite (disconnected graph?)")
         self.chi2 = out
         return out
@@ -404,5 +463,6 @@ def bench_c4(iterations=10, reps=3):
             "gn_plan_s": round(plan_s, 3), "gn_chi2_first_last": [float(chis[0]), float(chis[-1])],
             "gn_border_scalars": plan.nv - plan.nv_band,
             "gn_solver": "block cyclic reduction (Wb=%d)" % _abi.lib().slam_gn_bcr_block_rows(plan.nv_band, plan.W)
-            + (" + border Schur complement" if plan.nv_band < plan.nv else "")
+            + ((" + border Schur complement accumulated in the elimination (%d coupled blocks)" % len(plan.schur_blocks)
+                if plan.pslot is not None else " + border Schur complement") if plan.nv_band < plan.nv else "")
             if _abi.lib().slam_gn_bcr_block_rows(plan.nv_band, plan.W) > 0 else "band Cholesky"}

@@ -197,6 +197,27 @@ int slam_gn_iteration_bordered_f64(double* poses, int32_t N, const int32_t* ea,
                                    const int32_t* nbr_rows, int32_t n_nbr,
                                    double* work, double* out_chi2,
                                    int32_t* status, void* stream);
+/* The same bordered iteration with the border's Schur complement accumulated
+ * DURING the band's elimination: every eliminated
+ * block i with pslot[i] = k >= 0 (the blocks whose reduced rows couple to the
+ * border; slamhip.gn.GnPlan lists them symbolically) adds Y_i^T D_i^-1 Y_i to
+ * slot k of pwork (n_pslot x mc x mc doubles, mc = 16 ceil((nbd + 1) / 16)),
+ * the top block forms S and x_b = S^-1 s, and the back-substitution runs on
+ * one column.  Same result as slam_gn_iteration_bordered_f64 to rounding;
+ * needs the explicit-inverse cyclic reduction (SLAM_EINVAL otherwise).
+ * work: slam_gn_work_size_bordered(N, E, W, nv - nv_band) doubles. */
+int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea,
+                                const int32_t* eb, const double* tf,
+                                const double* w, int32_t E,
+                                const int32_t* node_col,
+                                const int32_t* slot_rc,
+                                const int32_t* slot_ptr,
+                                const int32_t* slot_items, int32_t n_slots,
+                                int32_t nv, int32_t W, int32_t nv_band,
+                                const int32_t* pslot, int32_t n_pslot,
+                                double* pwork, double* work,
+                                double* out_chi2, int32_t* status,
+                                void* stream);
 
 /* ---- occupancy grid (src/produce_occupancy_grid.py) ------------------------
  * pts: packed (x, y) scan points, scan_off (S+1), pose4 (S x 4: cos theta,

@@ -628,3 +628,110 @@ def test_plan_border_gated_by_solver_mode():
         lib.slam_gn_set_solver(0)
     p0 = gn.plan_for(len(guess), ea, eb)
     assert p0.nv - p0.nv_band == 27 and p0 is not p1
+
+
+def _bcr_schur_numpy(D, E, b, y, C, rb, nb):
+    """The Schur-accumulating bordered block cyclic reduction restated in NumPy
+    (eager updates; csrc/gn_bcr_gj.hip applies the same ones one level late):
+    returns (x_band, x_border, blocks whose reduced border rows were nonzero
+    at their elimination, in elimination order)."""
+    D = [d.copy() for d in D]
+    A = {}                       # couplings A[j, i] (row block j, column block i), both directions
+    for i in range(nb - 1):
+        A[(i + 1, i)] = E[i].copy()
+        A[(i, i + 1)] = E[i].T.copy()
+    R = [np.c_[b[i], y[i]] for i in range(nb)]   # [b_i | y_i]
+    S = C.copy()
+    s_ = rb.copy()
+    elim, zs, Xs, Ys, coupled = [], {}, {}, {}, []
+    s = 1
+    while s < nb:
+        for i in range(s, nb, 2 * s):
+            p, n = i - s, i + s
+            G = np.linalg.inv(D[i])
+            z = G @ R[i]
+            P = R[i].T @ z
+            if np.any(R[i][:, 1:] != 0):
+                coupled.append(i)
+            S -= P[1:, 1:]
+            s_ -= P[1:, 0]
+            zs[i] = z
+            Xs[i] = G @ A[(i, p)]
+            D[p] -= A[(p, i)] @ Xs[i]
+            R[p] = R[p] - A[(p, i)] @ z
+            if n < nb:
+                Ys[i] = G @ A[(i, n)]
+                D[n] -= A[(n, i)] @ Ys[i]
+                R[n] = R[n] - A[(n, i)] @ z
+                A[(n, p)] = -A[(n, i)] @ Xs[i]
+                A[(p, n)] = A[(n, p)].T
+            elim.append((s, i))
+        s *= 2
+    G0 = np.linalg.inv(D[0])
+    X0 = G0 @ R[0]
+    P0 = R[0].T @ X0
+    S -= P0[1:, 1:]
+    s_ -= P0[1:, 0]
+    xb = np.linalg.solve(S, s_)
+    x = {0: X0[:, 0] - X0[:, 1:] @ xb}
+    for (s, i) in reversed(elim):
+        p, n = i - s, i + s
+        v = zs[i][:, 0] - zs[i][:, 1:] @ xb - Xs[i] @ x[p]
+        if n < nb:
+            v = v - Ys[i] @ x[n]
+        x[i] = v
+    return np.concatenate([x[i] for i in range(nb)]), xb, coupled
+
+
+@pytest.mark.parametrize("nb,wb,nbd,seed", [(13, 4, 5, 0), (32, 3, 7, 1), (47, 2, 3, 2)])
+def test_schur_slots_match_a_numeric_reduction(nb, wb, nbd, seed):
+    """The symbolic list of border-coupled blocks (gn.schur_slots) equals the
+    blocks whose reduced border rows are nonzero in a numeric run of the
+    Schur-accumulating cyclic reduction, and that reduction (Schur complement
+    summed over the eliminated blocks, one-column back-substitution) solves
+    the bordered system: against np.linalg.solve at 1e-9."""
+    from unittest import mock
+
+    from slamhip import gn
+    rng = np.random.default_rng(seed)
+    n = nb * wb
+    D = [np.eye(wb) * 6 + (lambda m: m + m.T)(rng.normal(0, 0.3, (wb, wb))) for _ in range(nb)]
+    E = [rng.normal(0, 0.5, (wb, wb)) for _ in range(nb - 1)]
+    rows = np.r_[np.arange(wb + 1), np.arange(n - wb - 2, n)]   # the band's two ends couple to the border
+    Bm = np.zeros((n, nbd))
+    Bm[rows] = rng.normal(0, 0.4, (len(rows), nbd))
+    C = np.eye(nbd) * 8 + (lambda m: m + m.T)(rng.normal(0, 0.2, (nbd, nbd)))
+    H = np.zeros((n + nbd, n + nbd))
+    for i in range(nb):
+        H[i * wb:(i + 1) * wb, i * wb:(i + 1) * wb] = D[i]
+    for i in range(nb - 1):
+        H[(i + 1) * wb:(i + 2) * wb, i * wb:(i + 1) * wb] = E[i]
+        H[i * wb:(i + 1) * wb, (i + 1) * wb:(i + 2) * wb] = E[i].T
+    H[:n, n:] = Bm
+    H[n:, :n] = Bm.T
+    H[n:, n:] = C
+    rhs = rng.normal(0, 1, n + nbd)
+    want = np.linalg.solve(H, rhs)
+    b = [rhs[i * wb:(i + 1) * wb] for i in range(nb)]
+    y = [Bm[i * wb:(i + 1) * wb] for i in range(nb)]
+    xa, xb, coupled = _bcr_schur_numpy(D, E, b, y, C, rhs[n:], nb)
+    assert np.abs(np.r_[xa, xb] - want).max() <= 1e-9 * max(1.0, np.abs(want).max())
+
+    class FakeLib:
+        def slam_gn_bcr_block_rows(self, nv, W):
+            return wb
+    with mock.patch.object(gn._abi, "lib", lambda: FakeLib()):
+        pslot, blocks = gn.schur_slots(rows.astype(np.int32), n, wb)
+    assert blocks.tolist() == coupled
+    assert (pslot >= 0).sum() == len(coupled) and pslot[blocks].tolist() == list(range(len(blocks)))
+
+
+def test_c4_schur_plan_couples_few_blocks():
+    """C4's bordered plan: the border couples the band's two ends only, so six
+    eliminated blocks (one per level the last block's coupling climbs) carry
+    a Schur contribution, plus the top block."""
+    from slamhip import gn, synthetic
+    guess, ea, eb, tf, _ = synthetic.lap_graph_c4()
+    p = gn.GnPlan(len(guess), ea, eb)
+    assert p.nv - p.nv_band == 27 and p.pslot is not None
+    assert p.schur_blocks.tolist() == [467, 466, 464, 448, 384, 256]

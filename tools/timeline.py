@@ -1,8 +1,9 @@
-"""Per-pair timeline of one batched ICP launch (slam_icp_set_trace): for rank
-0's shard of the C3 stream, when each pair's workgroup started and ended in
-each scheduler phase, where (XCC / CU), and what bounds the makespan.  GPU only.
+"""Per-pair timeline of one batched ICP launch (slam_icp_set_trace): for a
+shard of the C3 stream (the 10k stream bench.py shards), when each pair's
+workgroup started and ended in each scheduler phase, where (XCC / CU), and
+what bounds the makespan.  GPU only.
 
-    python tools/timeline.py [pairs ...]        (default 1250 2500)
+    python tools/timeline.py [N:rank ...]     (default 8:0 4:0; a bare P: the first P pairs)
 """
 import os
 import sys
@@ -19,13 +20,27 @@ def main():
     from slamhip import _abi, se2, synthetic
     from slamhip import icp as k
     lib = _abi.lib()
-    sizes = [int(x) for x in sys.argv[1:]] or [1250, 2500]
-    n = max(sizes)
+    from slamhip import dist as sd
+    specs = sys.argv[1:] or ["8:0", "4:0"]
     seq = synthetic.make_sequence(10001, seed=2025)
-    inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, n + 1)])
-    ss = k.ScanSet(seq.scans[:n + 1])
-    for P in sizes:
-        b = k.IcpBatch(ss, np.arange(1, P + 1), np.arange(0, P), inits[:P], epsilon=0.05, max_iters=100)
+    inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, 10001)])
+    ss = k.ScanSet(seq.scans)
+    full = k.IcpBatch(ss, np.arange(1, 10001), np.arange(0, 10000), inits, epsilon=0.05, max_iters=100)
+    full.launch()
+    it_all = full.result().iters
+    np.save(os.path.join(REPO, "gpurun_out", "iters_10k.npy"), it_all)
+    for nr in (2, 4, 8):
+        mx = [int(it_all[sd.shard_range(10000, nr, r)[0]:sd.shard_range(10000, nr, r)[1]].max()) for r in range(nr)]
+        print(f"N{nr}: longest pair per shard (iterations) {mx}", flush=True)
+    for spec in specs:
+        if ":" in spec:
+            nr, r = (int(x) for x in spec.split(":"))
+            lo, hi, _ = sd.shard_range(10000, nr, r)
+        else:
+            lo, hi = 0, int(spec)
+        P = hi - lo
+        print(f"shard {spec}: pairs {lo}..{hi - 1}", flush=True)
+        b = k.IcpBatch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi], epsilon=0.05, max_iters=100)
         for _ in range(3):
             b.launch()
         torch.cuda.synchronize()
@@ -71,7 +86,7 @@ def main():
         grid = np.arange(0, np.nanmax(fin) + 50, 50)
         run = [int(np.sum((np.nan_to_num(st2, nan=1e18) <= g) & (np.nan_to_num(end2, nan=-1) > g))) for g in grid]
         print("   phase-2 pairs running every 50 us: " + " ".join(str(r) for r in run), flush=True)
-        np.save(os.path.join(REPO, "gpurun_out", f"timeline_{P}.npy"), t)
+        np.save(os.path.join(REPO, "gpurun_out", f"timeline_{spec.replace(':', '_')}.npy"), t)
 
 
 if __name__ == "__main__":

@@ -639,7 +639,11 @@ __global__ __launch_bounds__(kThreads) void top_schur_kernel(const double* __res
     double* Sm = X0 + WB * (mc + 1);  // [32][33]: S, then S^-1
     double* sv = Sm + 32 * 33;        // [32]: s
     double* xbs = sv + 32;            // [32]: x_b
-    const int tid = threadIdx.x;
+    double* P0 = xbs + 32;            // [32][33]: R_0^T X_0 (mc <= 32)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lk = lane >> 4;
+    constexpr int K4 = WB / 4;
     const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
     // the fused back-substitution's ready flags: cleared here (this launch
     // ends before it starts), block 0's set at the end
@@ -663,12 +667,37 @@ __global__ __launch_bounds__(kThreads) void top_schur_kernel(const double* __res
     }
     __syncthreads();
     if (gj_invert<T>(A, C) && tid == 0) *status = 1;   // ends with a barrier
-    for (int e = tid; e < WB * mc; e += kThreads) {
-        const int r = e / mc, c = e % mc;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int k = 0; k < WB; ++k) acc = fma(A[r * LDA + k], R[k * (mc + 1) + c], acc);
-        X0[r * (mc + 1) + c] = acc;
+    const int nct = mc / 16;
+    // X_0 = G_0 R_0 as MFMA tiles (wave w: tiles w, w + 4, ...), then
+    // P_0 = R_0^T X_0 (nct x nct tiles)
+    for (int t = wave; t < T * nct; t += 4) {
+        const int ti = t / nct, tc = t - ti * nct;
+        double af[K4], bf[K4];
+#pragma unroll
+        for (int k4 = 0; k4 < K4; ++k4) {
+            af[k4] = A[(16 * ti + lr) * LDA + 4 * k4 + lk];
+            bf[k4] = R[(4 * k4 + lk) * (mc + 1) + 16 * tc + lr];
+        }
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k4 = 0; k4 < K4; ++k4) acc = mma(af[k4], bf[k4], acc);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) X0[(16 * ti + lk + 4 * g) * (mc + 1) + 16 * tc + lr] = acc[g];
+    }
+    __syncthreads();
+    for (int t = wave; t < nct * nct; t += 4) {
+        const int ti = t / nct, tc = t - ti * nct;
+        double af[K4], bf[K4];
+#pragma unroll
+        for (int k4 = 0; k4 < K4; ++k4) {
+            af[k4] = R[(4 * k4 + lk) * (mc + 1) + 16 * ti + lr];
+            bf[k4] = X0[(4 * k4 + lk) * (mc + 1) + 16 * tc + lr];
+        }
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k4 = 0; k4 < K4; ++k4) acc = mma(af[k4], bf[k4], acc);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) P0[(16 * ti + lk + 4 * g) * 33 + 16 * tc + lr] = acc[g];
     }
     __syncthreads();
     // [S | s] entries e = k * (nbd + 1) + l (l = nbd: s), at most 4 per thread
@@ -697,10 +726,7 @@ __global__ __launch_bounds__(kThreads) void top_schur_kernel(const double* __res
                 for (int u = 0; u < 4; ++u) acc += pv[u];
             }
             for (; t < sc.n_slots; ++t) acc += sc.P[(static_cast<int64_t>(t) * mc + 1 + k) * mc + pc];
-            double p0 = 0.0;   // P_0 = R_0^T X_0
-#pragma unroll 8
-            for (int r = 0; r < WB; ++r) p0 = fma(R[r * (mc + 1) + 1 + k], X0[r * (mc + 1) + pc], p0);
-            acc += p0;
+            acc += P0[(1 + k) * 33 + pc];
             if (l < nbd) Sm[k * 33 + l] = cv - acc;
             else sv[k] = cv - acc;
         }
@@ -1229,7 +1255,7 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
         auto top_s_lds = [](int wb) {
             const int wc = wb > 32 ? wb : 32;
             return sizeof(double) * (static_cast<size_t>(wb) * (wb + 1) + static_cast<size_t>(wc) * 17 +
-                                     2 * static_cast<size_t>(wb) * 33 + 32 * 33 + 64);
+                                     2 * static_cast<size_t>(wb) * 33 + 2 * 32 * 33 + 64);
         };
         static bool attrs_s = false;
         if (!attrs_s) {

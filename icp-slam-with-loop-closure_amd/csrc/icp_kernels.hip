@@ -96,6 +96,13 @@ struct IcpArgs {
     uint2* qsave;
     float* dtsave;
     int32_t qsave_stride;
+    // launch order -> pair, XCD-aware (0: identity): with xcd_per = ceil(B / 8)
+    // and a grid of 8 * xcd_per workgroups, workgroup bx runs pair
+    // (bx % 8) * xcd_per + bx / 8, so each XCD (round-robin dispatch) walks a
+    // contiguous run of the stream and consecutive pairs, which share a scan
+    // (pc1 of pair i is pc2 of pair i + 1), stage it through the same L2
+    int32_t xcd_per;
+    int32_t n_pairs;   // pairs of the launch (the XCD-aware map's bound)
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
 #ifndef SLAM_TAIL_SHARE
@@ -893,8 +900,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         part = (bx >> 3) % parts;
         if (slot >= a.n_gangs) return;   // padding block (uniform)
     }
-    // pair of this workgroup: launch order or the scheduler's order
-    const int b = a.order ? a.order[slot] : slot;
+    // pair of this workgroup: launch order (XCD-aware when xcd_per > 0) or the
+    // scheduler's order
+    int b = a.order ? a.order[slot] : slot;
+    if (!GANG && !a.order && a.xcd_per > 0) {
+        b = (slot & 7) * a.xcd_per + (slot >> 3);
+        if (b >= a.n_pairs) return;   // padding workgroup (uniform)
+    }
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
@@ -2353,6 +2365,7 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
 // screen with exact chunk pruning (default).  Results are identical in all
 // three (tests/test_icp_gpu.py::test_nn_modes_identical).
 static thread_local int g_screen = 2;
+static thread_local int g_xcd_map = 1;   // XCD-aware pair map of order-free launches (diagnostics: 0 = identity)
 static thread_local unsigned long long* g_icp_stamps = nullptr;
 static thread_local unsigned long long* g_icp_evals = nullptr;
 static thread_local unsigned long long* g_icp_trace = nullptr;
@@ -2386,7 +2399,14 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
                             : (step ? inst->step : inst->batch);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds));
-    hipLaunchKernelGGL(fn, dim3(B), dim3(inst->block), lds, as_stream(stream), a);
+    int grid = B;
+    a.xcd_per = 0;
+    a.n_pairs = B;
+    if (!step && !a.order && g_xcd_map && B >= 64) {   // XCD-aware pair map (IcpArgs::xcd_per)
+        a.xcd_per = (B + 7) / 8;
+        grid = 8 * a.xcd_per;
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(inst->block), lds, as_stream(stream), a);
     return check_launch(step ? "icp_step kernel" : "icp_batch kernel");
 }
 
@@ -2425,6 +2445,7 @@ static thread_local int g_sched_heads = 64;
 // 3.12 ms without the exchange/head tiers and 3.40 ms with them, the 2,500-pair
 // shard 2.84 vs 2.31 ms, so the tiers start below 4,096 pairs
 constexpr int kHeadsMaxPairs = 4096;
+static thread_local int g_tiers_below = kHeadsMaxPairs;   // batches below this get the tail tiers
 
 static const Instance* pick_head_instance(int max_n1) {
     const Instance* best = nullptr;
@@ -2469,6 +2490,8 @@ static SideStream* side_stream(int dev) {
     if (dev < 0 || dev >= 64) return nullptr;
     SideStream& e = side[dev];
     if (!e.stream) {
+        // (round 5: the exchange tiers on the highest stream priority, the gangs
+        // on a side stream, measured slower: profiles/r05_shard_sweep2.txt)
         if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&e.stream2, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&e.stream3, hipStreamNonBlocking) != hipSuccess ||
@@ -2772,7 +2795,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const size_t nb = static_cast<size_t>(B);
     // tiers of phase 2: gangs (order[0, G)), CU-exclusive heads (order[G, H)),
     // the rest (order[H, B)) beside them
-    const int heads = g_sched_heads > 0 && B < kHeadsMaxPairs ? min(g_sched_heads, max(B / 16, 1)) : 0;
+    const int heads = g_sched_heads > 0 && B < g_tiers_below ? min(g_sched_heads, max(B / 16, 1)) : 0;
     // gang parts: g_sched_gang_parts workgroups per pair, or (0) teams: one
     // workgroup per 64-query group
     const bool team = g_sched_gang_parts == 0;
@@ -3000,6 +3023,19 @@ int slam_icp_set_schedule_warm(int on) {
 // workgroup (1, default) or as the three-kernel sort (0).  Same order.
 int slam_icp_set_sched_sort_one(int on) {
     g_sched_sort_one = on ? 1 : 0;
+    return ok();
+}
+// Diagnostics: batches of fewer than `pairs` pairs get the tail tiers (heads,
+// gangs, wide); 0 restores the default (4,096).
+// Diagnostics: the XCD-aware pair map of launches in stream order (1,
+// default) or the identity (0).  Results do not depend on it.
+int slam_icp_set_xcd_map(int on) {
+    g_xcd_map = on ? 1 : 0;
+    return ok();
+}
+int slam_icp_set_tier_limit(int pairs) {
+    if (pairs < 0) return fail(SLAM_EINVAL, "tier limit %d < 0", pairs);
+    g_tiers_below = pairs ? pairs : kHeadsMaxPairs;
     return ok();
 }
 int slam_icp_gang_timeouts(void) {

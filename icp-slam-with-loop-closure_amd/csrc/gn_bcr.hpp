@@ -14,7 +14,8 @@ struct BcrGjBufs {
     double *D, *E0, *E1, *Xs, *Ys, *SP, *SN;   // nb x Wb x Wb each
     double *bz, *SPb, *SNb, *x;                // nb x Wb x mc each (mc right-hand-side columns)
     double* bzo;                               // nb x Wb x mc: the odd blocks' z (Schur solves)
-    int32_t* ready;                            // nb: the fused back-substitution's flags
+    int32_t* ready;                            // [0]: the back-substitution's epoch (top kernel)
+    uint64_t* xg;                              // nb x 2 Wb: x as tagged granules (XCD-local back-substitution)
 };
 // A bordered solve with the border's Schur complement accumulated during the
 // elimination: the RHS block is [r_a | B] (mc

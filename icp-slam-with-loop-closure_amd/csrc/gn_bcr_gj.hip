@@ -645,9 +645,6 @@ __global__ __launch_bounds__(kThreads) void top_schur_kernel(const double* __res
     const int lr = lane & 15, lk = lane >> 4;
     constexpr int K4 = WB / 4;
     const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
-    // the fused back-substitution's ready flags: cleared here (this launch
-    // ends before it starts), block 0's set at the end
-    for (int j = tid + 1; j < nb; j += kThreads) ready[j] = 0;
     {
         double g[PER], a1[PER];
 #pragma unroll
@@ -746,7 +743,6 @@ __global__ __launch_bounds__(kThreads) void top_schur_kernel(const double* __res
         for (int k = 0; k < nbd; ++k) a = fma(X0[tid * (mc + 1) + 1 + k], xbs[k], a);
         x[tid] = X0[tid * (mc + 1)] - a;
     }
-    if (tid == 0) ready[0] = 1;
 }
 
 // Back-substitution of a Schur-accumulating bordered solve (one column):
@@ -892,30 +888,32 @@ __global__ __launch_bounds__(kThreads) void back_schur_kernel(const double* __re
 }
 
 // Every back-substitution level of a Schur-accumulating bordered solve in ONE
-// launch (a level is a few microseconds of load latency, a kernel boundary
-// another ~1.6 us, profiles/r05_launch_ubench.txt) — measured SLOWER (the
-// flags' cross-XCD release / acquire cost more than the launches), kept
-// selectable for A/B (SLAMHIP_GN_FUSED_BACK=1): workgroup w takes the w-th
-// odd block in coarsest-level-first order, waits until the x of its two
-// neighbours is published (ready[] flags: thread 0 polls with agent-scope
-// acquire loads, then a barrier), solves as back_schur_kernel and publishes
-// its own x (barrier, then an agent-scope release store).  Producers always
-// have lower workgroup indices than their consumers, and workgroups are
-// dispatched in index order, so the lowest unfinished one can always run.
-// top_schur_kernel zeroed the flags and set block 0's.  A wait longer than
-// `wait` s_memrealtime ticks sets *status = 2 and goes on (a wrong result that
+// launch, on ONE XCD (a level is ~1 us of load latency; as its own launch it
+// takes 4.8 us: profiles/r05_gn_kernel_stats.csv).  Only the workgroups with
+// blockIdx % 8 == 0 work — round-robin dispatch puts them all on the same XCD
+// (as the ICP gangs rely on), whose L2 is the one coherence point they need —
+// workgroup 8 w taking the w-th odd block in coarsest-level-first order.  A
+// block's x is published as data-tagged granules (tag 1 in the high word,
+// 32-bit halves of the doubles in the low; one relaxed
+// agent-scope store each, no fence: the data IS the flag, as in the ICP gang
+// exchange; the granules are zeroed by each iteration's linearisation
+// launch, so the tag is a constant) and its consumers poll them; block 0 (the
+// top launch's) is read plainly.  Producers have lower indices than their consumers and dispatch is
+// in index order, so the lowest unfinished block can always run.  A wait
+// longer than `wait` s_memrealtime ticks sets *status |= 2 (a wrong result
 // the caller reports, never a hang).
 template <int T>
-__global__ __launch_bounds__(kThreads) void back_schur_fused_kernel(const double* __restrict__ Xs,
-                                                                   const double* __restrict__ Ys,
-                                                                   const double* __restrict__ bzo,
-                                                                   double* x,
-                                                                   const double* __restrict__ xb, int32_t nbd,
-                                                                   int32_t nb, int32_t mc, int32_t* ready,
-                                                                   uint32_t wait, int32_t* __restrict__ status) {
+__global__ __launch_bounds__(kThreads) void back_schur_xcd_kernel(const double* __restrict__ Xs,
+                                                                 const double* __restrict__ Ys,
+                                                                 const double* __restrict__ bzo, double* x,
+                                                                 const double* __restrict__ xb, int32_t nbd,
+                                                                 int32_t nb, int32_t mc, uint64_t* xg, uint32_t wait,
+                                                                 int32_t* __restrict__ status) {
     constexpr int WB = 16 * T;
+    __shared__ uint32_t xh[2][2 * WB];   // the neighbours' x as 32-bit halves (lo, hi)
     const int tid = threadIdx.x;
-    int w = static_cast<int>(blockIdx.x);
+    if (blockIdx.x & 7) return;   // (uniform) not on the working XCD
+    int w = static_cast<int>(blockIdx.x >> 3);
     int s = 1;
     while (2 * s < nb) s *= 2;   // the top level
     for (;;) {
@@ -928,13 +926,13 @@ __global__ __launch_bounds__(kThreads) void back_schur_fused_kernel(const double
     if (i >= nb) return;   // (uniform) past the last odd block
     const int p = i - s, n = i + s;
     const bool hn = n < nb;
+    constexpr uint32_t ep = 1;   // the tag (granules zeroed by the linearisation launch)
     const int64_t B2 = static_cast<int64_t>(WB) * WB, RB = static_cast<int64_t>(WB) * mc;
     const int tr = tid >> 4, tc = tid & 15;
     const double* X = Xs + i * B2;
     const double* Y = Ys + i * B2;
     const int nzc = mc / 16;
-    // this block's own operands (written by earlier launches) in flight while
-    // thread 0 waits for the neighbours
+    // this block's own operands (earlier launches) in flight while the neighbours are polled
     double xv[T][T], yv[T][T], vp[T], vn[T], zv[T][2], cf[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -952,22 +950,39 @@ __global__ __launch_bounds__(kThreads) void back_schur_fused_kernel(const double
         for (int m = 0; m < 2; ++m)
             zv[u][m] = m < nzc ? bzo[i * RB + static_cast<int64_t>(tr + 16 * u) * mc + tc + 16 * m] : 0.0;
     }
-    if (tid == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(ready + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 ||
-               (hn && __hip_atomic_load(ready + n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0)) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > wait) {
-                atomicOr(status, 2);
-                break;
-            }
+    // the neighbours' x: granules (2 WB per block) polled until their tags are
+    // this iteration's; block 0 plain
+    for (int e = tid; e < 4 * WB; e += kThreads) {
+        const int side = e / (2 * WB), g = e - side * 2 * WB;
+        const int j = side ? n : p;
+        if (side && !hn) continue;
+        if (j == 0) {
+            const uint64_t bits = static_cast<uint64_t>(__double_as_longlong(x[g >> 1]));
+            xh[side][g] = static_cast<uint32_t>((g & 1) ? bits >> 32 : bits);
+            continue;
         }
+        const uint64_t* src = xg + static_cast<int64_t>(j) * 2 * WB + g;
+        uint64_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (static_cast<uint32_t>(v >> 32) != ep) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            do {
+                __builtin_amdgcn_s_sleep(1);
+                v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > wait) {
+                    atomicOr(status, 2);
+                    break;
+                }
+            } while (static_cast<uint32_t>(v >> 32) != ep);
+        }
+        xh[side][g] = static_cast<uint32_t>(v);
     }
     __syncthreads();
+    const double* xp_s = reinterpret_cast<const double*>(xh[0]);
+    const double* xn_s = reinterpret_cast<const double*>(xh[1]);
 #pragma unroll
-    for (int ww = 0; ww < T; ++ww) {   // the neighbours' x: after the acquire
-        vp[ww] = x[static_cast<int64_t>(p) * WB + tc + 16 * ww];
-        vn[ww] = hn ? x[static_cast<int64_t>(n) * WB + tc + 16 * ww] : 0.0;
+    for (int ww = 0; ww < T; ++ww) {
+        vp[ww] = xp_s[tc + 16 * ww];
+        vn[ww] = hn ? xn_s[tc + 16 * ww] : 0.0;
     }
     double v[T];
 #pragma unroll
@@ -987,14 +1002,20 @@ __global__ __launch_bounds__(kThreads) void back_schur_fused_kernel(const double
         v[u] += dpp_row<0x124>(v[u]);
         v[u] += dpp_row<0x128>(v[u]);
     }
-    if (tc == 0) {
+    // lanes tc = 0 / 1 of each row publish the lo / hi granule of its rows
+    // (every lane of the row holds the row sum); tc = 0 also writes x
+    if (tc < 2) {
+        const uint64_t tag = static_cast<uint64_t>(ep) << 32;
+        uint64_t* dst = xg + static_cast<int64_t>(i) * 2 * WB;
 #pragma unroll
-        for (int u = 0; u < T; ++u) x[static_cast<int64_t>(i) * WB + tr + 16 * u] = -v[u];
+        for (int u = 0; u < T; ++u) {
+            const int r = tr + 16 * u;
+            const uint64_t bits = static_cast<uint64_t>(__double_as_longlong(-v[u]));
+            if (tc == 0) x[static_cast<int64_t>(i) * WB + r] = -v[u];
+            __hip_atomic_store(dst + 2 * r + tc, tag | (tc ? bits >> 32 : bits & 0xffffffffull), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    // every wave's x stores made visible at agent scope, then one flag
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(ready + i, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Bordered solves: x_i = z_i - X_i x_p - Y_i x_n for WB x mc blocks (row
@@ -1167,12 +1188,14 @@ BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc) {
     b.x = b.SNb + nb * RB;
     b.bzo = b.x + nb * RB;
     b.ready = reinterpret_cast<int32_t*>(b.bzo + nb * RB);
+    b.xg = reinterpret_cast<uint64_t*>(b.bzo + nb * RB + (nb + 1) / 2 + 1);
     return b;
 }
 
 int64_t bcr_gj_work_size(int32_t nv, int32_t Wb, int32_t mc) {
     const int64_t nb = (nv + Wb - 1) / Wb;
-    return 7 * nb * Wb * Wb + 5 * nb * Wb * static_cast<int64_t>(mc) + nb;   // + the ready flags
+    // + the epoch word (ready) and the back-substitution's tagged granules
+    return 7 * nb * Wb * Wb + 5 * nb * Wb * static_cast<int64_t>(mc) + (nb + 1) / 2 + 1 + 2 * nb * Wb;
 }
 
 // The levels of the explicit-inverse reduction, after bcr_load_kernel filled
@@ -1286,22 +1309,25 @@ int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const
 
 int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st, const BcrSchur* sc) {
     const int nb = (nv + Wb - 1) / Wb;
-    // measured and off by default: the flag hand-offs (agent-scope release /
-    // acquire across XCDs) cost more than the launches they replace
-    // (profiles/r05_gn_ab_schur.txt: 2,926-2,949 against 5,282-5,310 it/s)
+    // off by default: the XCD-local tagged hand-offs gain 1.5 % at C4
+    // (profiles/r05_gn_ab_xcdback.txt: 5,455-5,463 against 5,370-5,392 it/s)
+    // and rest on the round-robin workgroup -> XCD dispatch (a violated
+    // assumption times out: status 2, an error, never a wrong answer); the
+    // first form (flags with agent-scope release / acquire across XCDs) was
+    // slower than the launches (2,926-2,949 it/s, profiles/r05_gn_ab_schur.txt)
     static const bool fused = [] {
         const char* e = getenv("SLAMHIP_GN_FUSED_BACK");
         return e && e[0] == '1';
     }();
-    if (sc && fused && nb > 1) {   // every level in one launch (ready flags)
-        using BackFFn = void (*)(const double*, const double*, const double*, double*, const double*, int32_t, int32_t,
-                                 int32_t, int32_t*, uint32_t, int32_t*);
-        static const BackFFn backfs[6] = {bcrgj::back_schur_fused_kernel<1>, bcrgj::back_schur_fused_kernel<2>,
-                                          bcrgj::back_schur_fused_kernel<3>, bcrgj::back_schur_fused_kernel<4>,
-                                          bcrgj::back_schur_fused_kernel<5>, bcrgj::back_schur_fused_kernel<6>};
-        hipLaunchKernelGGL(backfs[Wb / 16 - 1], dim3(nb - 1), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bzo, b.x,
-                           sc->xb, sc->nbd, nb, mc, b.ready, static_cast<uint32_t>(10000000), sc->status);
-        return check_launch("gn bcr (explicit inverse, Schur border) fused back-substitution");
+    if (sc && fused && nb > 1) {   // every level in one launch on one XCD (tagged granules)
+        using BackXFn = void (*)(const double*, const double*, const double*, double*, const double*, int32_t, int32_t,
+                                 int32_t, uint64_t*, uint32_t, int32_t*);
+        static const BackXFn backxs[6] = {bcrgj::back_schur_xcd_kernel<1>, bcrgj::back_schur_xcd_kernel<2>,
+                                          bcrgj::back_schur_xcd_kernel<3>, bcrgj::back_schur_xcd_kernel<4>,
+                                          bcrgj::back_schur_xcd_kernel<5>, bcrgj::back_schur_xcd_kernel<6>};
+        hipLaunchKernelGGL(backxs[Wb / 16 - 1], dim3(8 * (nb - 1)), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bzo,
+                           b.x, sc->xb, sc->nbd, nb, mc, b.xg, static_cast<uint32_t>(20000000), sc->status);
+        return check_launch("gn bcr (explicit inverse, Schur border) XCD-local back-substitution");
     }
     if (sc) {   // one column: z_i[:, 0] - z_i[:, B] x_b
         using BackSFn = void (*)(const double*, const double*, const double*, double*, const double*, int32_t, int32_t,

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kGnLinBlock) void gn_linearize_kernel(
     const double* __restrict__ poses, const int32_t* __restrict__ ea, const int32_t* __restrict__ eb,
     const double* __restrict__ tf, const double* __restrict__ w, int32_t E, double* __restrict__ contrib,
     double* __restrict__ chi2p, double* __restrict__ z0, int64_t nz0, double* __restrict__ z1, int64_t nz1,
-    double* __restrict__ z2, int64_t nz2) {
+    double* __restrict__ z2, int64_t nz2, double* __restrict__ z3, int64_t nz3) {
     __shared__ double red[kGnLinBlock / 64];
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     {
@@ -139,6 +139,7 @@ __global__ __launch_bounds__(kGnLinBlock) void gn_linearize_kernel(
         zero_doubles(z0, nz0, e, stride);
         zero_doubles(z1, nz1, e, stride);
         zero_doubles(z2, nz2, e, stride);
+        zero_doubles(z3, nz3, e, stride);
     }
     // workgroups past the edges only zero (the grid is sized for the zeroing)
     if (static_cast<int64_t>(blockIdx.x) * blockDim.x >= E) return;   // uniform
@@ -812,14 +813,22 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
     const int64_t nz0 = bd.D ? 2 * bd.nb * B2 : static_cast<int64_t>(nv_band) * (W + 1);
     const int64_t nz1 = bd.D ? static_cast<int64_t>(bd.nb) * Wb * mc : 0;
     const int64_t nBR = static_cast<int64_t>(nbd) * nv;
+    // the Schur path's back-substitution granules (gn_bcr_gj.hip back_schur_xcd_kernel), zeroed every iteration
+    double* z3 = nullptr;
+    int64_t nz3 = 0;
+    if (nbd > 0 && pslot && bd.D) {
+        const BcrGjBufs g = bcr_gj_bufs(bwork, nv_band, Wb, mc);
+        z3 = reinterpret_cast<double*>(g.xg);
+        nz3 = 2 * static_cast<int64_t>(bd.nb) * Wb;
+    }
     const bool fold = E > 0;
     const int n_chi2p = (E + kGnLinBlock - 1) / kGnLinBlock;   // chi2 partials (in chi2e: n_chi2p <= E)
     // enough workgroups for the zeroing too (about 16 double2 stores per thread)
-    const int64_t nzero = (nz0 + nz1 + nBR) / 2;
+    const int64_t nzero = (nz0 + nz1 + nBR + nz3) / 2;
     const int lin_grid = static_cast<int>(std::max<int64_t>(n_chi2p, std::min<int64_t>((nzero / 16 + kGnLinBlock - 1) / kGnLinBlock, 2048)));
     if (E > 0)
         hipLaunchKernelGGL(gn_linearize_kernel, dim3(lin_grid), dim3(kGnLinBlock), 0, s, poses, ea, eb, tf, w, E,
-                           contrib, chi2e, z0, nz0, bd.bz, nz1, BR, nBR);
+                           contrib, chi2e, z0, nz0, bd.bz, nz1, BR, nBR, z3, nz3);
     if (nv == 0 || n_slots <= 0) hipLaunchKernelGGL(gn_chi2_kernel, dim3(1), dim3(256), 0, s, chi2e, n_chi2p, out_chi2);
     if (nv == 0) return check_launch("gn kernels");
     if (!fold && hipMemsetAsync(z0, 0, sizeof(double) * static_cast<size_t>(nz0), s) != hipSuccess)

@@ -96,12 +96,12 @@ struct IcpArgs {
     uint2* qsave;
     float* dtsave;
     int32_t qsave_stride;
-    // launch order -> pair, XCD-aware (0: identity): with xcd_per = ceil(B / 8)
-    // and a grid of 8 * xcd_per workgroups, workgroup bx runs pair
-    // (bx % 8) * xcd_per + bx / 8, so each XCD (round-robin dispatch) walks a
-    // contiguous run of the stream and consecutive pairs, which share a scan
-    // (pc1 of pair i is pc2 of pair i + 1), stage it through the same L2
-    int32_t xcd_per;
+    // launch order -> pair, XCD-aware (0: identity): runs of xcd_run
+    // consecutive pairs go to one XCD (round-robin dispatch: workgroup bx runs
+    // on XCD bx % 8), so consecutive pairs, which share a scan (pc1 of pair i
+    // is pc2 of pair i + 1), stage it through the same L2; the runs rotate
+    // over the XCDs, so a stretch of slow pairs still spreads over the chip
+    int32_t xcd_run;
     int32_t n_pairs;   // pairs of the launch (the XCD-aware map's bound)
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
@@ -903,8 +903,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     // pair of this workgroup: launch order (XCD-aware when xcd_per > 0) or the
     // scheduler's order
     int b = a.order ? a.order[slot] : slot;
-    if (!GANG && !a.order && a.xcd_per > 0) {
-        b = (slot & 7) * a.xcd_per + (slot >> 3);
+    if (!GANG && !a.order && a.xcd_run > 0) {
+        const int k = slot >> 3, g = a.xcd_run;
+        b = ((k / g) * 8 + (slot & 7)) * g + k % g;
         if (b >= a.n_pairs) return;   // padding workgroup (uniform)
     }
     const int tid = threadIdx.x;
@@ -2365,7 +2366,9 @@ __global__ __launch_bounds__(kKabschBlock) void kabsch_kernel(const double2* __r
 // screen with exact chunk pruning (default).  Results are identical in all
 // three (tests/test_icp_gpu.py::test_nn_modes_identical).
 static thread_local int g_screen = 2;
-static thread_local int g_xcd_map = 1;   // XCD-aware pair map of order-free launches (diagnostics: 0 = identity)
+// XCD-aware pair map of order-free launches: runs of this many consecutive
+// pairs per XCD (0 = identity; diagnostics)
+static thread_local int g_xcd_map = 16;
 static thread_local unsigned long long* g_icp_stamps = nullptr;
 static thread_local unsigned long long* g_icp_evals = nullptr;
 static thread_local unsigned long long* g_icp_trace = nullptr;
@@ -2400,11 +2403,11 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds));
     int grid = B;
-    a.xcd_per = 0;
+    a.xcd_run = 0;
     a.n_pairs = B;
-    if (!step && !a.order && g_xcd_map && B >= 64) {   // XCD-aware pair map (IcpArgs::xcd_per)
-        a.xcd_per = (B + 7) / 8;
-        grid = 8 * a.xcd_per;
+    if (!step && !a.order && g_xcd_map > 0 && B >= 64) {   // XCD-aware pair map (IcpArgs::xcd_run)
+        a.xcd_run = g_xcd_map;
+        grid = (B + 8 * g_xcd_map - 1) / (8 * g_xcd_map) * 8 * g_xcd_map;
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(inst->block), lds, as_stream(stream), a);
     return check_launch(step ? "icp_step kernel" : "icp_batch kernel");
@@ -3027,10 +3030,12 @@ int slam_icp_set_sched_sort_one(int on) {
 }
 // Diagnostics: batches of fewer than `pairs` pairs get the tail tiers (heads,
 // gangs, wide); 0 restores the default (4,096).
-// Diagnostics: the XCD-aware pair map of launches in stream order (1,
-// default) or the identity (0).  Results do not depend on it.
-int slam_icp_set_xcd_map(int on) {
-    g_xcd_map = on ? 1 : 0;
+// Diagnostics: the XCD-aware pair map of launches in stream order: runs of
+// `run` consecutive pairs per XCD (default 16; 0 = identity; -1 restores the
+// default).  Results do not depend on it.
+int slam_icp_set_xcd_map(int run) {
+    if (run < -1 || run > 4096) return fail(SLAM_EINVAL, "xcd map run %d", run);
+    g_xcd_map = run < 0 ? 16 : run;
     return ok();
 }
 int slam_icp_set_tier_limit(int pairs) {

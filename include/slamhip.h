@@ -309,10 +309,11 @@ int slam_icp_set_sched_sort_one(int on);
 /* Diagnostics: batches of fewer than `pairs` pairs get the scheduler's tail
  * tiers (heads, gangs, wide); 0 restores the default (4,096). */
 int slam_icp_set_tier_limit(int pairs);
-/* Diagnostics: the XCD-aware pair map of launches in stream order (1,
- * default: each XCD walks a contiguous run of pairs, so consecutive pairs
- * share their common scan through one L2) or the identity (0). */
-int slam_icp_set_xcd_map(int on);
+/* Diagnostics: the XCD-aware pair map of launches in stream order: runs of
+ * `run` consecutive pairs per XCD (default 16, so consecutive pairs share
+ * their common scan through one L2 while the runs rotate over the XCDs),
+ * 0 the identity, -1 the default. */
+int slam_icp_set_xcd_map(int run);
 int slam_gn_set_stamps(void* dev_buf);
 /* GN linear solver (per host thread): 0 auto (block cyclic reduction when the
  * band allows it), 1 band Cholesky, 2 block cyclic reduction (falls back to 1

@@ -1,4 +1,5 @@
-"""Interleaved A/B of the XCD-aware pair map (slam_icp_set_xcd_map) on the
+"""Interleaved A/B of the XCD-aware pair map (slam_icp_set_xcd_map, runs of
+XCD_RUNS consecutive pairs per XCD; 0 = identity) on the
 10k C3 batch and the N = 8 / 4 shards of the same stream: HIP events, median
 of 5 launches per setting per round, 4 rounds.  GPU only."""
 import os
@@ -26,10 +27,11 @@ def main():
         cases[f"{nr}:{r}"] = (lo, hi)
     batches = {n: k.IcpBatch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi], epsilon=0.05,
                              max_iters=100) for n, (lo, hi) in cases.items()}
-    res = {(n, m): [] for n in cases for m in (0, 1)}
+    runs = [int(x) for x in os.environ.get("XCD_RUNS", "16,0,4,64").split(",")]
+    res = {(n, m): [] for n in cases for m in runs}
     ref = {}
     for rnd in range(4):
-        for m in (1, 0):
+        for m in runs:
             lib.slam_icp_set_xcd_map(m)
             for n, b in batches.items():
                 b.launch()
@@ -47,10 +49,10 @@ def main():
                 if n not in ref:
                     ref[n] = r
                 assert np.array_equal(r.tf, ref[n].tf) and np.array_equal(r.iters, ref[n].iters), (n, m)
-    lib.slam_icp_set_xcd_map(1)
+    lib.slam_icp_set_xcd_map(-1)
     for n in cases:
-        print(f"{n:6s} xcd map ON  " + " ".join(f"{t:.3f}" for t in res[(n, 1)]) + f"  | OFF " +
-              " ".join(f"{t:.3f}" for t in res[(n, 0)]), flush=True)
+        print(f"{n:6s} " + " | ".join(f"run {m}: " + " ".join(f"{t:.3f}" for t in res[(n, m)]) for m in runs),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ inst = int(os.environ.get("SLAMHIP_INSTANCE", "-1"))
 lib = _abi.lib()
 lib.slam_icp_force_instance(inst)
 lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
-lib.slam_icp_set_xcd_map(int(os.environ.get("SLAMHIP_XCD_MAP", "1")))
+lib.slam_icp_set_xcd_map(int(os.environ.get("SLAMHIP_XCD_MAP", "-1")))
 seq = synthetic.make_sequence(pairs + 1, seed=2025)
 inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, pairs + 1)])
 ss = k.ScanSet(seq.scans)

@@ -61,7 +61,7 @@ def main():
             assert lib.slam_icp_set_schedule(v[5] if len(v) > 5 else -1, 1024) == 0
             assert lib.slam_icp_set_sched_sort_one(v[6] if len(v) > 6 else 1) == 0
             assert lib.slam_icp_set_tier_limit(v[7] if len(v) > 7 else 0) == 0
-            assert lib.slam_icp_set_xcd_map(v[8] if len(v) > 8 else 1) == 0
+            assert lib.slam_icp_set_xcd_map(v[8] if len(v) > 8 else -1) == 0
             line = []
             t1 = None
             for n in [1] + ranks:
@@ -87,7 +87,7 @@ def main():
         lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_sched_sort_one(1)
         lib.slam_icp_set_tier_limit(0)
-        lib.slam_icp_set_xcd_map(1)
+        lib.slam_icp_set_xcd_map(-1)
 
 
 if __name__ == "__main__":

@@ -103,6 +103,11 @@ struct IcpArgs {
     // over the XCDs, so a stretch of slow pairs still spreads over the chip
     int32_t xcd_run;
     int32_t n_pairs;   // pairs of the launch (the XCD-aware map's bound)
+    // angle pre-tier (launch_batch): slots below *skip_lt of an ordered launch
+    // belong to pairs another tier runs (NULL: none); an order entry < 0 is
+    // padding (both: the workgroup leaves at once)
+    const int32_t* skip_lt;
+    const int32_t* take_lt;   // wide tier: slots at or past *take_lt leave at once (NULL: none)
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
 #ifndef SLAM_TAIL_SHARE
@@ -903,6 +908,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     // pair of this workgroup: launch order (XCD-aware when xcd_per > 0) or the
     // scheduler's order
     int b = a.order ? a.order[slot] : slot;
+    if (a.order && (b < 0 || (a.skip_lt && slot < *a.skip_lt))) return;   // (uniform) another tier's pair / padding
     if (!GANG && !a.order && a.xcd_run > 0) {
         const int k = slot >> 3, g = a.xcd_run;
         b = ((k / g) * 8 + (slot & 7)) * g + k % g;
@@ -1469,6 +1475,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
     const int part = (bx >> 3) % parts;   // = the query group of this workgroup
     if (slot >= a.n_gangs) return;
     const int b = a.order ? a.order[slot] : slot;
+    if (b < 0) return;   // padding (uniform)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1917,8 +1924,9 @@ __device__ __forceinline__ KabschOut kabsch_from_sums(double tot, const SE2& T, 
 // the wave) instead of LDS broadcasts (1 KB to VGPRs per ds_read_b128).
 __global__ __launch_bounds__(256) void wide_prep_kernel(IcpArgs a, float2* __restrict__ wcand) {
     const int slot = blockIdx.x;
-    if (slot >= a.n_gangs) return;
+    if (slot >= a.n_gangs || (a.take_lt && slot >= *a.take_lt)) return;
     const int b = a.order ? a.order[slot] : slot;
+    if (b < 0) return;   // padding (uniform)
     const int s2 = a.dst_scan[b];
     const int64_t o2 = a.scan_off[s2];
     const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
@@ -1950,8 +1958,9 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
     const int bx = static_cast<int>(blockIdx.x);
     const int slot = (bx / (8 * parts)) * 8 + (bx & 7);   // a pair's workgroups on one XCD
     const int part = (bx >> 3) % parts;                     // = its 64-query group
-    if (slot >= a.n_gangs) return;
+    if (slot >= a.n_gangs || (a.take_lt && slot >= *a.take_lt)) return;
     const int b = a.order ? a.order[slot] : slot;
+    if (b < 0) return;   // padding (uniform)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int it0 = 0;
@@ -2482,6 +2491,12 @@ static thread_local int g_sched_warm = 0;
 // batches of <= kSortOneMax pairs sort on one workgroup (diagnostics: 0 = the
 // three-kernel sort at every size)
 static thread_local int g_sched_sort_one = 1;
+// Angle pre-tier (batches below the tier limit): up to g_angle_max pairs whose
+// initial transform turns by more than g_angle_thresh rad — the C3 stream's
+// long pairs all start at a turn of 0.5-3 rad — run on
+// the wide tier from the start, beside phase 1 of the others (0: off)
+static thread_local int g_angle_max = 0;
+static thread_local float g_angle_thresh = 0.3f;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
@@ -2722,10 +2737,23 @@ __global__ __launch_bounds__(kSortBlock) void sched_scatter_kernel(const int32_t
 // The workgroup also zeroes `nz` words at `zero` (the phase-2 exchange slots:
 // no separate memset on the boundary).
 constexpr int kSortOneMax = 4096;
+// MODE 0: the phase boundary's sort (sched_bucket) of the pairs ids[koff ..
+// B) (koff = *k_dev, 0 without; ids NULL: the pairs 0 .. B-1), order[] = the
+// sorted pairs then -1 padding up to B.  MODE 1: the angle pre-tier's order
+// (launch_batch): pairs whose initial transform turns by more than `thresh`
+// rad first, largest turn first (32 buckets per rad... 255 over [0, pi]), the
+// rest in index order; *k_dev = min(#turning pairs, kmax); those pairs'
+// out_iters are set to 0 ("not started": the repair launch runs them from
+// their initial transform if their tier timed out).
+template <int MODE>
 __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_t* __restrict__ iters,
                                                                     const float* __restrict__ key, int32_t B,
                                                                     float thresh, int32_t* __restrict__ order,
-                                                                    uint64_t* __restrict__ zero, int64_t nz) {
+                                                                    uint64_t* __restrict__ zero, int64_t nz,
+                                                                    const int32_t* __restrict__ ids,
+                                                                    int32_t* __restrict__ k_dev,
+                                                                    const double* __restrict__ init, int32_t kmax,
+                                                                    int32_t* __restrict__ out_iters) {
     constexpr int WAVES = kSortBlock / 64;
     constexpr int PER = kSortOneMax / kSortBlock;
     __shared__ int base[kNB];
@@ -2733,13 +2761,26 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int64_t e = tid; e < nz; e += kSortBlock) zero[e] = 0;
     for (int i = tid; i < kNB; i += kSortBlock) base[i] = 0;
+    const int koff = (MODE == 0 && k_dev) ? *k_dev : 0;
+    const int n = B - koff;   // entries sorted
     __syncthreads();
-    int q[PER];
+    int q[PER], pb[PER];
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
-        const int b = c * kSortBlock + tid;
-        q[c] = b < B ? sched_bucket(iters, key, b, thresh) : -1;
-        if (q[c] >= 0) atomicAdd(&base[q[c]], 1);
+        const int j = c * kSortBlock + tid;
+        pb[c] = j < n ? (ids ? ids[koff + j] : j) : -1;
+        q[c] = -1;
+        if (pb[c] >= 0) {
+            if constexpr (MODE == 0) {
+                q[c] = sched_bucket(iters, key, pb[c], thresh);
+            } else {
+                const double* t = init + 9 * static_cast<int64_t>(pb[c]);
+                const float ang = fabsf(atan2f(static_cast<float>(t[3]), static_cast<float>(t[0])));
+                q[c] = ang > thresh ? min(max(255 - static_cast<int>(ang * (255.0f / 3.14159265f)), 0), 255)
+                                    : kSchedBuckets;
+            }
+            atomicAdd(&base[q[c]], 1);
+        }
     }
     __syncthreads();
     if (tid < 64) {   // exclusive scan of the kNB totals by wave 0 (chunks of 64 + a running carry)
@@ -2756,11 +2797,15 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
             if (i < kNB) base[i] = carry + x - v;
             carry += __shfl(x, 63, 64);
         }
+        if constexpr (MODE == 1) {
+            if (lane == 0) *k_dev = min(base[kSchedBuckets], kmax);   // turning pairs precede bucket 256
+        }
     }
     __syncthreads();
+    const int kk = MODE == 1 ? min(base[kSchedBuckets], kmax) : 0;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
-        if (c * kSortBlock >= B) break;   // uniform
+        if (c * kSortBlock >= n) break;   // uniform
         for (int i = tid; i < WAVES * kNB; i += kSortBlock) cnt[i] = 0;
         __syncthreads();
         const bool valid = q[c] >= 0;
@@ -2777,7 +2822,8 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
         if (valid) {
             int pos = base[q[c]] + rank;
             for (int w = 0; w < wave; ++w) pos += cnt[w * kNB + q[c]];
-            order[pos] = c * kSortBlock + tid;
+            order[pos] = pb[c];
+            if (MODE == 1 && pos < kk) out_iters[pb[c]] = 0;
         }
         __syncthreads();
         // the chunk's totals advance the running offsets (one thread per bucket)
@@ -2787,6 +2833,9 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
             base[i] += t;
         }
         __syncthreads();
+    }
+    if constexpr (MODE == 0) {
+        for (int j = n + tid; j < B; j += kSortBlock) order[j] = -1;   // padding: those workgroups leave at once
     }
 }
 
@@ -2809,7 +2858,13 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const int wide_parts = (max_n1 + 63) / 64;
     const bool wide_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap && wide_parts <= kTeamMaxParts &&
                          wide_lds_bytes(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) <= kMaxLds;
-    const int Wd = wide_ok ? min(g_sched_wide, heads) : 0;
+    // angle pre-tier: the turning pairs on the wide tier from the start (its
+    // stream, stream3, is then busy: no phase-2 wide tier)
+    const int ap = (g_angle_max > 0 && wide_ok && B < g_tiers_below && B <= kSortOneMax && g_sched_sort_one &&
+                    B >= g_bulk_gang_below)
+                       ? min(g_angle_max, B)
+                       : 0;
+    const int Wd = wide_ok && ap == 0 ? min(g_sched_wide, heads) : 0;
     const int G = gang_ok ? max(0, min(g_sched_gangs, heads - Wd)) : 0;
     const size_t wide_slot_words = static_cast<size_t>(Wd) * 2 * wide_parts * 32;
     const size_t gang_slot_bytes =
@@ -2829,7 +2884,13 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const size_t qsave_bytes = g_sched_warm ? (nb * static_cast<size_t>(max_n1) * sizeof(uint2) + nb * 8 * sizeof(float) +
                                                255) / 256 * 256
                                            : 0;
-    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes;
+    // angle pre-tier: order0 (B), its count (device), exchange slots, fp32 candidates
+    const size_t cand_cap_w = static_cast<size_t>(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk);
+    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * wide_parts * 32;
+    const size_t ap_bytes = ap ? ((nb + 1) * sizeof(int32_t) + 255) / 256 * 256 + ap_slot_words * sizeof(uint64_t) +
+                                     static_cast<size_t>(ap) * cand_cap_w * sizeof(float2)
+                               : 0;
+    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes + ap_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);   // hist_blk[nblk][kNB]
@@ -2840,6 +2901,11 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     float2* wide_cand = reinterpret_cast<float2*>(static_cast<char*>(ws) + sched_bytes + gang_slot_bytes);
     uint64_t* bulk_slots =
         reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes + gang_slot_bytes + wide_cand_bytes);
+    char* ap0 = static_cast<char*>(ws) + sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes;
+    int32_t* order0 = ap ? reinterpret_cast<int32_t*>(ap0) : nullptr;   // [B] + the count at order0[B]
+    int32_t* ap_k = ap ? order0 + nb : nullptr;
+    uint64_t* ap_slots = ap ? reinterpret_cast<uint64_t*>(ap0 + ((nb + 1) * sizeof(int32_t) + 255) / 256 * 256) : nullptr;
+    float2* ap_cand = ap ? reinterpret_cast<float2*>(ap_slots + ap_slot_words) : nullptr;
     IcpArgs a = args;
     a.phase_cap = probe;
     a.sched_key = key;
@@ -2849,8 +2915,31 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         a.dtsave = reinterpret_cast<float*>(q0 + nb * static_cast<size_t>(max_n1) * sizeof(uint2));
         a.qsave_stride = max_n1;
     }
-    int rc;
-    if (bg) {
+    int rc = 0;
+    SideStream* side0 = nullptr;
+    if (ap) {
+        // the turning pairs first in order0 (their out_iters set to 0: not
+        // started), then the wide tier for them from their initial transforms on
+        // stream3, launched before phase 1 so that its workgroups reach the CUs
+        // first; phase 1 runs the rest (order0 from *ap_k on)
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) side0 = side_stream(dev);
+        if (!side0) return (void)hipFreeAsync(ws, s), fail(SLAM_EHIP, "icp scheduler: side streams");
+        hipLaunchKernelGGL(sched_sort_one_kernel<1>, dim3(1), dim3(kSortBlock), 0, s, args.out_iters,
+                           static_cast<const float*>(nullptr), B, g_angle_thresh, order0, ap_slots,
+                           static_cast<int64_t>(ap_slot_words), static_cast<const int32_t*>(nullptr), ap_k, args.init, ap,
+                           args.out_iters);
+        if (hipEventRecord(side0->fork, s) != hipSuccess || hipStreamWaitEvent(side0->stream3, side0->fork, 0) != hipSuccess)
+            rc = fail(SLAM_EHIP, "icp scheduler: fork");
+        IcpArgs w = args;
+        w.order = order0;
+        w.take_lt = ap_k;
+        if (rc == 0) rc = launch_wide(w, ap, max_n1, max_n2, side0->stream3, ap_slots, ap_cand);
+        a.order = order0;
+        a.skip_lt = ap_k;
+    }
+    if (rc != 0) {
+    } else if (bg) {
         // a phase-1 gang that timed out writes nothing: its pair must then read
         // as "not started" (out_iters 0) in phase 2, never as a stale result
         (void)hipMemsetAsync(args.out_iters, 0, nb * sizeof(int32_t), s);
@@ -2866,8 +2955,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         if (bg) (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
         if (B <= kSortOneMax && g_sched_sort_one) {
             // one launch on the phase boundary: the sort, and the exchange slots zeroed beside it
-            hipLaunchKernelGGL(sched_sort_one_kernel, dim3(1), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
-                               order, gang_slots, static_cast<int64_t>(G + Wd > 0 ? gang_slot_bytes / sizeof(uint64_t) : 0));
+            hipLaunchKernelGGL(sched_sort_one_kernel<0>, dim3(1), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
+                               order, gang_slots, static_cast<int64_t>(G + Wd > 0 ? gang_slot_bytes / sizeof(uint64_t) : 0),
+                               order0, ap_k, static_cast<const double*>(nullptr), 0, static_cast<int32_t*>(nullptr));
         } else {
             if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
             hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
@@ -2881,11 +2971,12 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         a.phase_cap = 0;
         a.resume = 1;
         a.order = order;
+        a.skip_lt = nullptr;
         const int GW = Wd + G;   // pairs on the exchange tiers (wide, then gangs)
         const Instance* hinst = heads > GW && g_forced_instance < 0 ? pick_head_instance(max_n1) : nullptr;
         int dev = 0;
         SideStream* side = nullptr;
-        if ((hinst || GW > 0 || bg) && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
+        if ((hinst || GW > 0 || bg || ap) && max_n2 <= kCandCap && hipGetDevice(&dev) == hipSuccess) side = side_stream(dev);
         if (side) {
             // fork: the gangs and the head pairs on CU-exclusive workgroups first
             // (the GPU is empty after the scheduler kernels: they take the first
@@ -2931,9 +3022,18 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 r.order = order;
                 rc = launch(false, r, bg ? B : GW, max_n1, max_n2, stream);
             }
+            if (rc == 0 && ap) {   // the same for the angle pre-tier (not started: from the initial transform)
+                IcpArgs r = a;
+                r.order = order0;
+                rc = launch(false, r, ap, max_n1, max_n2, stream);
+            }
         } else {
             rc = launch(false, a, B, max_n1, max_n2, stream);
         }
+    }
+    if (ap && side0 && rc != 0) {   // an error after the pre-tier's fork: still join its stream before the free
+        (void)hipEventRecord(side0->join3, side0->stream3);
+        (void)hipStreamWaitEvent(s, side0->join3, 0);
     }
     (void)hipFreeAsync(ws, s);
     return rc;
@@ -3038,6 +3138,16 @@ int slam_icp_set_xcd_map(int run) {
     g_xcd_map = run < 0 ? 16 : run;
     return ok();
 }
+// Angle pre-tier (see launch_batch): batches below the tier limit run up to
+// `max_pairs` pairs whose initial transform turns by more than `thresh_rad`
+// on the wide tier from the start (0: off).  Results are bit-identical.
+int slam_icp_set_angle_tier(int max_pairs, float thresh_rad) {
+    if (max_pairs < 0 || max_pairs > 256 || !(thresh_rad >= 0.0f))
+        return fail(SLAM_EINVAL, "angle tier: %d pairs, threshold %g", max_pairs, static_cast<double>(thresh_rad));
+    g_angle_max = max_pairs;
+    g_angle_thresh = thresh_rad;
+    return ok();
+}
 int slam_icp_set_tier_limit(int pairs) {
     if (pairs < 0) return fail(SLAM_EINVAL, "tier limit %d < 0", pairs);
     g_tiers_below = pairs ? pairs : kHeadsMaxPairs;
@@ -3068,8 +3178,10 @@ int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float
     if (!iters || !key || !order) return fail(SLAM_EINVAL, "null array argument");
     hipStream_t s = as_stream(stream);
     if (B <= kSortOneMax) {   // the one-workgroup sort launch_batch uses at this size
-        hipLaunchKernelGGL(sched_sort_one_kernel, dim3(1), dim3(kSortBlock), 0, s, iters, key, B, thresh, order,
-                           static_cast<uint64_t*>(nullptr), static_cast<int64_t>(0));
+        hipLaunchKernelGGL(sched_sort_one_kernel<0>, dim3(1), dim3(kSortBlock), 0, s, iters, key, B, thresh, order,
+                           static_cast<uint64_t*>(nullptr), static_cast<int64_t>(0), static_cast<const int32_t*>(nullptr),
+                           static_cast<int32_t*>(nullptr), static_cast<const double*>(nullptr), 0,
+                           static_cast<int32_t*>(nullptr));
         return check_launch("sched sort kernel");
     }
     const int nblk = (B + kSortBlock - 1) / kSortBlock;

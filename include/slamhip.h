@@ -309,6 +309,11 @@ int slam_icp_set_sched_sort_one(int on);
 /* Diagnostics: batches of fewer than `pairs` pairs get the scheduler's tail
  * tiers (heads, gangs, wide); 0 restores the default (4,096). */
 int slam_icp_set_tier_limit(int pairs);
+/* Diagnostics: the angle pre-tier — batches below the tier limit run up to
+ * `max_pairs` pairs whose initial transform turns by more than `thresh_rad`
+ * on the wide tier from the start, beside the two-phase schedule of the
+ * others (0: off).  Results are bit-identical. */
+int slam_icp_set_angle_tier(int max_pairs, float thresh_rad);
 /* Diagnostics: the XCD-aware pair map of launches in stream order: runs of
  * `run` consecutive pairs per XCD (default 16, so consecutive pairs share
  * their common scan through one L2 while the runs rotate over the XCDs),

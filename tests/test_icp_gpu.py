@@ -15,6 +15,7 @@ from conftest import case_arrays, homog
 pytestmark = pytest.mark.gpu
 TOL = 1e-9
 DEFAULT_GANGS = (24, 4)   # the library's scheduler defaults (restored after a test changes them)
+DEFAULT_ANGLE = (0, 0.3)
 DEFAULT_WIDE = (0, 1)
 DEFAULT_BULK = (0, 2)
 
@@ -447,6 +448,15 @@ def test_gangs_are_bit_identical(k):
                                                              history=True)
             assert lib.slam_icp_gang_timeouts() == 0
         assert lib.slam_icp_set_schedule_wide(0, 1) == 0
+        # the angle pre-tier: the turning pairs on the wide tier from their
+        # initial transforms, beside phase 1 of the rest (with gangs, with heads only)
+        for amax, athr, gangs in ((24, 0.3, 24), (64, 0.05, 24), (8, 0.3, 0)):
+            assert lib.slam_icp_set_schedule_gangs(gangs, 4) == 0
+            assert lib.slam_icp_set_angle_tier(amax, athr) == 0
+            runs[("angle", amax, athr, gangs)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100,
+                                                             history=True)
+            assert lib.slam_icp_gang_timeouts() == 0
+        assert lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE) == 0
         # bulk gangs: both phases' bulk as gangs of 2 / 3 ordinary workgroups
         for parts in (2, 3):
             assert lib.slam_icp_set_bulk_gangs(4096, parts) == 0
@@ -464,6 +474,7 @@ def test_gangs_are_bit_identical(k):
         lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
         lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
+        lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE)
     assert single.iters.max() > 30
     for key, r in runs.items():
         assert np.array_equal(r.iters, single.iters), key
@@ -491,10 +502,12 @@ def test_gang_timeouts_are_repaired(k):
         assert lib.slam_icp_set_schedule(-1, 1024) == 0
         assert lib.slam_icp_set_gang_wait(1) == 0
         lib.slam_icp_gang_timeouts()   # clear
-        for gangs, parts, wide, bulk in ((64, 4, 0, 0), (16, 0, 0, 0), (0, 4, 16, 0), (8, 4, 0, 2), (0, 4, 0, 3)):
+        for gangs, parts, wide, bulk, angle in ((64, 4, 0, 0, 0), (16, 0, 0, 0, 0), (0, 4, 16, 0, 0), (8, 4, 0, 2, 0),
+                                                (0, 4, 0, 3, 0), (0, 4, 0, 0, 16)):
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
             assert lib.slam_icp_set_schedule_wide(wide, 1) == 0
             assert lib.slam_icp_set_bulk_gangs(4096 if bulk else 0, max(bulk, 2)) == 0
+            assert lib.slam_icp_set_angle_tier(angle, 0.1) == 0
             r = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() > 0, (gangs, parts, wide)
             assert np.array_equal(r.iters, single.iters), (gangs, parts)
@@ -507,6 +520,7 @@ def test_gang_timeouts_are_repaired(k):
         lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
         lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
+        lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE)
     assert lib.slam_icp_gang_timeouts() == 0
 
 

@@ -2456,6 +2456,12 @@ static thread_local int g_sched_heads = 64;
 // round 4 (probe 3, profiles/r04_strong_probe.txt): the 5,000-pair shard runs
 // 3.12 ms without the exchange/head tiers and 3.40 ms with them, the 2,500-pair
 // shard 2.84 vs 2.31 ms, so the tiers start below 4,096 pairs
+#ifndef SLAM_AUTO_ANGLE
+#define SLAM_AUTO_ANGLE 24
+#endif
+#ifndef SLAM_AUTO_SHARE
+#define SLAM_AUTO_SHARE 2
+#endif
 constexpr int kHeadsMaxPairs = 4096;
 static thread_local int g_tiers_below = kHeadsMaxPairs;   // batches below this get the tail tiers
 
@@ -2497,6 +2503,18 @@ static thread_local int g_sched_sort_one = 1;
 // the wide tier from the start, beside phase 1 of the others (0: off)
 static thread_local int g_angle_max = 0;
 static thread_local float g_angle_thresh = 0.3f;
+// Automatic tier profile by batch size (the default; any explicit tier setter
+// turns it off, slam_icp_set_schedule_auto(1) turns it back on), measured on
+// every rank's shard of the 10k C3 stream (tools/shard_sweep.py,
+// profiles/r05_shard_sweep*.txt):
+//   B <  kAutoSmall (8-rank shards): the angle pre-tier, kAutoAngle pairs on
+//        wide workgroups sharing a CU kAutoShare ways, no phase-2 tiers;
+//   B <  the tier limit (4-rank shards): 64 heads, the first 24 as gangs of 4;
+//   larger batches: no tiers.
+static thread_local int g_sched_auto = 1;
+constexpr int kAutoSmall = 2048;
+constexpr int kAutoAngle = SLAM_AUTO_ANGLE;
+constexpr int kAutoShare = SLAM_AUTO_SHARE;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
@@ -2600,7 +2618,7 @@ static int launch_bulk_gangs(const IcpArgs& args, int B, const BulkGangInstance*
 // W pairs (args.order[0..W)) on the wide tier: one workgroup per 64-query
 // group, the parts of a pair on one XCD (slots as launch_gangs).
 static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipStream_t s, uint64_t* slots,
-                       float2* wcand) {
+                       float2* wcand, int share) {
     const int parts = (max_n1 + 63) / 64;
     if (max_n2 > kCandCap || parts < 1 || parts > kTeamMaxParts) return fail(SLAM_EINVAL, "icp wide tier: shape");
     IcpArgs a = args;
@@ -2613,7 +2631,7 @@ static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipSt
     a.gang_wait = g_gang_wait;
     const size_t need = wide_lds_bytes(a.cand_cap);
     if (need > kMaxLds) return fail(SLAM_EINVAL, "icp wide tier: LDS");
-    const size_t lds = max(need, kMaxLds / static_cast<size_t>(max(g_wide_share, 1)));
+    const size_t lds = max(need, kMaxLds / static_cast<size_t>(max(share, 1)));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(icp_wide_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds));
     hipLaunchKernelGGL(wide_prep_kernel, dim3(W), dim3(256), 0, s, a, wcand);
@@ -2847,11 +2865,29 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const size_t nb = static_cast<size_t>(B);
     // tiers of phase 2: gangs (order[0, G)), CU-exclusive heads (order[G, H)),
     // the rest (order[H, B)) beside them
-    const int heads = g_sched_heads > 0 && B < g_tiers_below ? min(g_sched_heads, max(B / 16, 1)) : 0;
-    // gang parts: g_sched_gang_parts workgroups per pair, or (0) teams: one
-    // workgroup per 64-query group
-    const bool team = g_sched_gang_parts == 0;
-    const int parts = team ? (max_n1 + 63) / 64 : g_sched_gang_parts;
+    // the tier profile: explicit settings, or the automatic one by batch size
+    int cfg_heads = g_sched_heads, cfg_gangs = g_sched_gangs, cfg_parts = g_sched_gang_parts;
+    int cfg_wide = g_sched_wide, cfg_share = g_wide_share, cfg_angle = g_angle_max;
+    if (g_sched_auto) {
+        cfg_wide = 0;
+        cfg_share = 1;
+        cfg_parts = 4;
+        if (B < kAutoSmall) {
+            cfg_heads = 0;
+            cfg_gangs = 0;
+            cfg_angle = kAutoAngle;
+            cfg_share = kAutoShare;
+        } else {
+            cfg_heads = 64;
+            cfg_gangs = 24;
+            cfg_angle = 0;
+        }
+    }
+    const int heads = cfg_heads > 0 && B < g_tiers_below ? min(cfg_heads, max(B / 16, 1)) : 0;
+    // gang parts: cfg_parts workgroups per pair, or (0) teams: one workgroup
+    // per 64-query group
+    const bool team = cfg_parts == 0;
+    const int parts = team ? (max_n1 + 63) / 64 : cfg_parts;
     const bool gang_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap &&
                          (team ? parts <= kTeamMaxParts : parts >= 2 && pick_gang_instance(max_n1, parts) != nullptr);
     // tiers of phase 2: wide (order[0, Wd)), gangs (order[Wd, Wd + G)), heads, bulk
@@ -2860,12 +2896,12 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                          wide_lds_bytes(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) <= kMaxLds;
     // angle pre-tier: the turning pairs on the wide tier from the start (its
     // stream, stream3, is then busy: no phase-2 wide tier)
-    const int ap = (g_angle_max > 0 && wide_ok && B < g_tiers_below && B <= kSortOneMax && g_sched_sort_one &&
+    const int ap = (cfg_angle > 0 && wide_ok && B < g_tiers_below && B <= kSortOneMax && g_sched_sort_one &&
                     B >= g_bulk_gang_below)
-                       ? min(g_angle_max, B)
+                       ? min(cfg_angle, B)
                        : 0;
-    const int Wd = wide_ok && ap == 0 ? min(g_sched_wide, heads) : 0;
-    const int G = gang_ok ? max(0, min(g_sched_gangs, heads - Wd)) : 0;
+    const int Wd = wide_ok && ap == 0 ? min(cfg_wide, heads) : 0;
+    const int G = gang_ok ? max(0, min(cfg_gangs, heads - Wd)) : 0;
     const size_t wide_slot_words = static_cast<size_t>(Wd) * 2 * wide_parts * 32;
     const size_t gang_slot_bytes =
         (static_cast<size_t>(G) * 2 * max(parts, 1) * 32 + wide_slot_words) * sizeof(uint64_t);
@@ -2934,7 +2970,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         IcpArgs w = args;
         w.order = order0;
         w.take_lt = ap_k;
-        if (rc == 0) rc = launch_wide(w, ap, max_n1, max_n2, side0->stream3, ap_slots, ap_cand);
+        if (rc == 0) rc = launch_wide(w, ap, max_n1, max_n2, side0->stream3, ap_slots, ap_cand, cfg_share);
         a.order = order0;
         a.skip_lt = ap_k;
     }
@@ -2989,7 +3025,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 hipStreamWaitEvent(side->stream3, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
             // the wide tier on its own stream (the gangs must not queue behind it)
-            if (rc == 0 && Wd > 0) rc = launch_wide(a, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand);
+            if (rc == 0 && Wd > 0) rc = launch_wide(a, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand, cfg_share);
             if (rc == 0 && G > 0) {
                 IcpArgs g = a;
                 g.order = order + Wd;
@@ -3084,6 +3120,7 @@ int slam_icp_set_eval_counter(void* dev_u64) {
 int slam_icp_set_schedule_heads(int heads) {
     if (heads < 0) return fail(SLAM_EINVAL, "schedule: negative head count");
     g_sched_heads = heads;
+    g_sched_auto = 0;
     return ok();
 }
 int slam_icp_set_schedule_gangs(int gangs, int parts) {
@@ -3091,6 +3128,7 @@ int slam_icp_set_schedule_gangs(int gangs, int parts) {
         return fail(SLAM_EINVAL, "schedule: gangs %d parts %d", gangs, parts);
     g_sched_gangs = gangs;
     g_sched_gang_parts = parts;
+    g_sched_auto = 0;
     return ok();
 }
 // Gang parts that timed out waiting for a partner since the last call (their
@@ -3103,6 +3141,7 @@ int slam_icp_set_schedule_wide(int pairs, int share) {
     if (pairs < 0 || share < 1 || share > 8) return fail(SLAM_EINVAL, "schedule: wide %d share %d", pairs, share);
     g_sched_wide = pairs;
     g_wide_share = share;
+    g_sched_auto = 0;
     return ok();
 }
 // Bulk gangs: batches of fewer than `below_pairs` pairs (>= the scheduler's
@@ -3146,6 +3185,23 @@ int slam_icp_set_angle_tier(int max_pairs, float thresh_rad) {
         return fail(SLAM_EINVAL, "angle tier: %d pairs, threshold %g", max_pairs, static_cast<double>(thresh_rad));
     g_angle_max = max_pairs;
     g_angle_thresh = thresh_rad;
+    g_sched_auto = 0;
+    return ok();
+}
+// The automatic tier profile by batch size (1, default) or the explicit
+// settings (0; any tier setter selects them).  1 also restores the explicit
+// settings' defaults (64 heads, 24 gangs of 4, no wide tier, no angle tier).
+int slam_icp_set_schedule_auto(int on) {
+    g_sched_auto = on ? 1 : 0;
+    if (on) {
+        g_sched_heads = 64;
+        g_sched_gangs = 24;
+        g_sched_gang_parts = 4;
+        g_sched_wide = 0;
+        g_wide_share = 1;
+        g_angle_max = 0;
+        g_angle_thresh = 0.3f;
+    }
     return ok();
 }
 int slam_icp_set_tier_limit(int pairs) {

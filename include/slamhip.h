@@ -314,6 +314,11 @@ int slam_icp_set_tier_limit(int pairs);
  * on the wide tier from the start, beside the two-phase schedule of the
  * others (0: off).  Results are bit-identical. */
 int slam_icp_set_angle_tier(int max_pairs, float thresh_rad);
+/* The scheduler's automatic tier profile by batch size (1, default: the angle
+ * pre-tier below 2,048 pairs, heads + gangs below 4,096, none above; DESIGN.md
+ * section 6) or the explicit settings (0).  Any of the tier setters above
+ * selects the explicit settings; 1 restores their defaults too. */
+int slam_icp_set_schedule_auto(int on);
 /* Diagnostics: the XCD-aware pair map of launches in stream order: runs of
  * `run` consecutive pairs per XCD (default 16, so consecutive pairs share
  * their common scan through one L2 while the runs rotate over the XCDs),

@@ -14,8 +14,7 @@ from conftest import case_arrays, homog
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-9
-DEFAULT_GANGS = (24, 4)   # the library's scheduler defaults (restored after a test changes them)
-DEFAULT_ANGLE = (0, 0.3)
+DEFAULT_ANGLE = (0, 0.3)   # the explicit settings' defaults (slam_icp_set_schedule_auto(1) restores the automatic profile)
 DEFAULT_WIDE = (0, 1)
 DEFAULT_BULK = (0, 2)
 
@@ -381,7 +380,7 @@ def test_schedule_is_invisible(k):
         ref_ro = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=6, rotation_only=True)
     finally:
         lib.slam_icp_set_schedule(-1, 1024)
-        lib.slam_icp_set_schedule_heads(64)
+        lib.slam_icp_set_schedule_auto(1)
     a = outs[0]
     assert a.iters.min() < 8 < a.iters.max()
     for o in outs[1:-1]:
@@ -411,7 +410,7 @@ def test_default_schedule_large_batch(k):
         single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100)
     finally:
         lib.slam_icp_set_schedule(-1, 1024)
-        lib.slam_icp_set_schedule_heads(64)
+        lib.slam_icp_set_schedule_auto(1)
     assert phased.iters.max() > 5
     assert np.array_equal(plain.iters, single.iters)
     assert np.array_equal(plain.tf, single.tf) and np.array_equal(plain.err, single.err)
@@ -471,10 +470,8 @@ def test_gangs_are_bit_identical(k):
         assert lib.slam_icp_set_schedule_gangs(1, 1) != 0   # a gang needs two parts
     finally:
         lib.slam_icp_set_schedule(-1, 1024)
-        lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
-        lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
-        lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE)
+        lib.slam_icp_set_schedule_auto(1)
     assert single.iters.max() > 30
     for key, r in runs.items():
         assert np.array_equal(r.iters, single.iters), key
@@ -517,10 +514,8 @@ def test_gang_timeouts_are_repaired(k):
     finally:
         lib.slam_icp_set_gang_wait(0)
         lib.slam_icp_set_schedule(-1, 1024)
-        lib.slam_icp_set_schedule_gangs(*DEFAULT_GANGS)
-        lib.slam_icp_set_schedule_wide(*DEFAULT_WIDE)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
-        lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE)
+        lib.slam_icp_set_schedule_auto(1)
     assert lib.slam_icp_gang_timeouts() == 0
 
 

@@ -75,9 +75,7 @@ def main():
                 out.append(f"{P}:{np.median(ts):.3f}{'' if same else '!'}")
             print(f"h,g,k,w,s,bb,bp,probe {st:22s} " + " ".join(out), flush=True)
     finally:
-        lib.slam_icp_set_schedule_heads(64)
-        lib.slam_icp_set_schedule_gangs(24, 4)
-        lib.slam_icp_set_schedule_wide(0, 1)
+        lib.slam_icp_set_schedule_auto(1)
         lib.slam_icp_set_bulk_gangs(0, 2)
         lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_schedule_warm(0)

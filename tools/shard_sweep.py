@@ -7,7 +7,7 @@ projected N-GPU time is the slowest shard (bench.py takes the max over ranks).
 draws its noise after the whole trajectory, so a shorter stream is not a
 prefix of the 10k one.)  GPU only.
 
-    python tools/shard_sweep.py [setting ...]
+    python tools/shard_sweep.py [setting ... | auto]
 """
 import os
 import sys
@@ -53,16 +53,22 @@ def main():
         return float(np.median(ts))
     try:
         for st in settings:
-            v = [int(x) for x in st.split(",")]
+            if st == "auto":   # the library's automatic tier profile by batch size
+                assert lib.slam_icp_set_schedule_auto(1) == 0
+                v = [0, 0, 4, 0, 1]
+            else:
+                v = [int(x) for x in st.split(",")]
             h, g, gp, w, ws = v[:5]
-            assert lib.slam_icp_set_schedule_heads(h) == 0
-            assert lib.slam_icp_set_schedule_gangs(g, gp) == 0
-            assert lib.slam_icp_set_schedule_wide(w, ws) == 0
+            if st != "auto":
+                assert lib.slam_icp_set_schedule_heads(h) == 0
+                assert lib.slam_icp_set_schedule_gangs(g, gp) == 0
+                assert lib.slam_icp_set_schedule_wide(w, ws) == 0
             assert lib.slam_icp_set_schedule(v[5] if len(v) > 5 else -1, 1024) == 0
             assert lib.slam_icp_set_sched_sort_one(v[6] if len(v) > 6 else 1) == 0
             assert lib.slam_icp_set_tier_limit(v[7] if len(v) > 7 else 0) == 0
             assert lib.slam_icp_set_xcd_map(v[8] if len(v) > 8 else -1) == 0
-            assert lib.slam_icp_set_angle_tier(v[9] if len(v) > 9 else 0, (v[10] if len(v) > 10 else 30) / 100.0) == 0
+            if st != "auto":
+                assert lib.slam_icp_set_angle_tier(v[9] if len(v) > 9 else 0, (v[10] if len(v) > 10 else 30) / 100.0) == 0
             line = []
             t1 = None
             for n in [1] + ranks:
@@ -82,9 +88,7 @@ def main():
                 line.append(f"N{n}: max {mx:.3f} ({t1 / mx:.2f}x) shards " + " ".join(f"{t:.3f}" for t in ts))
             print(f"h,g,k,w,s {st:16s} | " + " | ".join(line), flush=True)
     finally:
-        lib.slam_icp_set_schedule_heads(64)
-        lib.slam_icp_set_schedule_gangs(24, 4)
-        lib.slam_icp_set_schedule_wide(0, 1)
+        lib.slam_icp_set_schedule_auto(1)
         lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_sched_sort_one(1)
         lib.slam_icp_set_tier_limit(0)

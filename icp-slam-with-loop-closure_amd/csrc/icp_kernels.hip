@@ -908,7 +908,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     // pair of this workgroup: launch order (XCD-aware when xcd_per > 0) or the
     // scheduler's order
     int b = a.order ? a.order[slot] : slot;
-    if (a.order && (b < 0 || (a.skip_lt && slot < *a.skip_lt))) return;   // (uniform) another tier's pair / padding
+    if (a.order && (b < 0 || (a.skip_lt && slot < *a.skip_lt) || (a.take_lt && slot >= *a.take_lt)))
+        return;   // (uniform) another tier's pair / padding
     if (!GANG && !a.order && a.xcd_run > 0) {
         const int k = slot >> 3, g = a.xcd_run;
         b = ((k / g) * 8 + (slot & 7)) * g + k % g;
@@ -2503,16 +2504,23 @@ static thread_local int g_sched_sort_one = 1;
 // the wide tier from the start, beside phase 1 of the others (0: off)
 static thread_local int g_angle_max = 0;
 static thread_local float g_angle_thresh = 0.3f;
+// the pre-tier's kind: 0 the wide tier (g_wide_share workgroups per CU), or
+// 2 / 3: bulk gangs of that many ordinary workgroups (cheap enough for the
+// larger shards' dozens of turning pairs)
+static thread_local int g_angle_kind = 0;
 // Automatic tier profile by batch size (the default; any explicit tier setter
 // turns it off, slam_icp_set_schedule_auto(1) turns it back on), measured on
 // every rank's shard of the 10k C3 stream (tools/shard_sweep.py,
 // profiles/r05_shard_sweep*.txt):
 //   B <  kAutoSmall (8-rank shards): the angle pre-tier, kAutoAngle pairs on
 //        wide workgroups sharing a CU kAutoShare ways, no phase-2 tiers;
-//   B <  the tier limit (4-rank shards): 64 heads, the first 24 as gangs of 4;
+//   B <= kSortOneMax (4- and 2-rank shards): the angle pre-tier as bulk gangs
+//        of 3 (kAutoMidAngle pairs) and, in phase 2, 64 heads, the first 24 as
+//        gangs of 4 (5,000 pairs: 2.76 ms against 3.77 with the heads alone);
 //   larger batches: no tiers.
 static thread_local int g_sched_auto = 1;
 constexpr int kAutoSmall = 2048;
+constexpr int kAutoMidAngle = 48;
 constexpr int kAutoAngle = SLAM_AUTO_ANGLE;
 constexpr int kAutoShare = SLAM_AUTO_SHARE;
 
@@ -2754,7 +2762,7 @@ __global__ __launch_bounds__(kSortBlock) void sched_scatter_kernel(const int32_t
 // running offset plus its rank among the chunk's earlier pairs of that bucket.
 // The workgroup also zeroes `nz` words at `zero` (the phase-2 exchange slots:
 // no separate memset on the boundary).
-constexpr int kSortOneMax = 4096;
+constexpr int kSortOneMax = 8192;
 // MODE 0: the phase boundary's sort (sched_bucket) of the pairs ids[koff ..
 // B) (koff = *k_dev, 0 without; ids NULL: the pairs 0 .. B-1), order[] = the
 // sorted pairs then -1 padding up to B.  MODE 1: the angle pre-tier's order
@@ -2867,23 +2875,31 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     // the rest (order[H, B)) beside them
     // the tier profile: explicit settings, or the automatic one by batch size
     int cfg_heads = g_sched_heads, cfg_gangs = g_sched_gangs, cfg_parts = g_sched_gang_parts;
-    int cfg_wide = g_sched_wide, cfg_share = g_wide_share, cfg_angle = g_angle_max;
+    int cfg_wide = g_sched_wide, cfg_share = g_wide_share, cfg_angle = g_angle_max, cfg_akind = g_angle_kind;
+    int tiers_below = g_tiers_below;
     if (g_sched_auto) {
         cfg_wide = 0;
         cfg_share = 1;
         cfg_parts = 4;
+        cfg_akind = 0;
         if (B < kAutoSmall) {
             cfg_heads = 0;
             cfg_gangs = 0;
             cfg_angle = kAutoAngle;
             cfg_share = kAutoShare;
-        } else {
+        } else if (B <= kSortOneMax) {
             cfg_heads = 64;
             cfg_gangs = 24;
+            cfg_angle = kAutoMidAngle;
+            cfg_akind = 3;
+            tiers_below = kSortOneMax + 1;
+        } else {
+            cfg_heads = 0;
+            cfg_gangs = 0;
             cfg_angle = 0;
         }
     }
-    const int heads = cfg_heads > 0 && B < g_tiers_below ? min(cfg_heads, max(B / 16, 1)) : 0;
+    const int heads = cfg_heads > 0 && B < tiers_below ? min(cfg_heads, max(B / 16, 1)) : 0;
     // gang parts: cfg_parts workgroups per pair, or (0) teams: one workgroup
     // per 64-query group
     const bool team = cfg_parts == 0;
@@ -2896,8 +2912,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                          wide_lds_bytes(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) <= kMaxLds;
     // angle pre-tier: the turning pairs on the wide tier from the start (its
     // stream, stream3, is then busy: no phase-2 wide tier)
-    const int ap = (cfg_angle > 0 && wide_ok && B < g_tiers_below && B <= kSortOneMax && g_sched_sort_one &&
-                    B >= g_bulk_gang_below)
+    const BulkGangInstance* apg = cfg_akind >= 2 ? pick_bulk_gang_instance(max_n1, cfg_akind) : nullptr;
+    const int ap = (cfg_angle > 0 && (cfg_akind >= 2 ? apg != nullptr : wide_ok) && B <= kSortOneMax &&
+                    g_sched_sort_one && B >= g_bulk_gang_below)
                        ? min(cfg_angle, B)
                        : 0;
     const int Wd = wide_ok && ap == 0 ? min(cfg_wide, heads) : 0;
@@ -2922,7 +2939,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                                            : 0;
     // angle pre-tier: order0 (B), its count (device), exchange slots, fp32 candidates
     const size_t cand_cap_w = static_cast<size_t>(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk);
-    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * wide_parts * 32;
+    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * max(wide_parts, 3) * 32;
     const size_t ap_bytes = ap ? ((nb + 1) * sizeof(int32_t) + 255) / 256 * 256 + ap_slot_words * sizeof(uint64_t) +
                                      static_cast<size_t>(ap) * cand_cap_w * sizeof(float2)
                                : 0;
@@ -2970,7 +2987,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         IcpArgs w = args;
         w.order = order0;
         w.take_lt = ap_k;
-        if (rc == 0) rc = launch_wide(w, ap, max_n1, max_n2, side0->stream3, ap_slots, ap_cand, cfg_share);
+        if (rc == 0)
+            rc = apg ? launch_bulk_gangs(w, ap, apg, max_n2, side0->stream3, ap_slots)
+                     : launch_wide(w, ap, max_n1, max_n2, side0->stream3, ap_slots, ap_cand, cfg_share);
         a.order = order0;
         a.skip_lt = ap_k;
     }
@@ -3181,10 +3200,18 @@ int slam_icp_set_xcd_map(int run) {
 // `max_pairs` pairs whose initial transform turns by more than `thresh_rad`
 // on the wide tier from the start (0: off).  Results are bit-identical.
 int slam_icp_set_angle_tier(int max_pairs, float thresh_rad) {
-    if (max_pairs < 0 || max_pairs > 256 || !(thresh_rad >= 0.0f))
+    if (max_pairs < 0 || max_pairs > 1024 || !(thresh_rad >= 0.0f))
         return fail(SLAM_EINVAL, "angle tier: %d pairs, threshold %g", max_pairs, static_cast<double>(thresh_rad));
     g_angle_max = max_pairs;
     g_angle_thresh = thresh_rad;
+    g_sched_auto = 0;
+    return ok();
+}
+// The angle pre-tier's kind: 0 the wide tier, 2 / 3 bulk gangs of that many
+// ordinary workgroups per pair.
+int slam_icp_set_angle_tier_kind(int kind) {
+    if (kind != 0 && kind != 2 && kind != 3) return fail(SLAM_EINVAL, "angle tier kind %d not in {0, 2, 3}", kind);
+    g_angle_kind = kind;
     g_sched_auto = 0;
     return ok();
 }
@@ -3201,6 +3228,7 @@ int slam_icp_set_schedule_auto(int on) {
         g_wide_share = 1;
         g_angle_max = 0;
         g_angle_thresh = 0.3f;
+        g_angle_kind = 0;
     }
     return ok();
 }

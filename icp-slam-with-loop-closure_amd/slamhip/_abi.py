@@ -42,6 +42,7 @@ SIGNATURES = {
     "slam_icp_set_xcd_map": (c_int, [c_int]),
     "slam_icp_set_angle_tier": (c_int, [c_int, ctypes.c_float]),
     "slam_icp_set_schedule_auto": (c_int, [c_int]),
+    "slam_icp_set_angle_tier_kind": (c_int, [c_int]),
     "slam_icp_set_eval_counter": (c_int, [c_ptr]),
     "slam_icp_set_trace": (c_int, [c_ptr]),
     "slam_icp_status": (c_int, [c_ptr]),
@@ -73,6 +74,9 @@ SIGNATURES = {
     "slam_gn_iteration_schur_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                             c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                             c_ptr, c_ptr]),
+    "slam_gn_iterations_schur_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
+                                             c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
+                                             c_ptr, c_int, c_ptr]),
 }
 
 

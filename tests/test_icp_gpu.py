@@ -449,13 +449,17 @@ def test_gangs_are_bit_identical(k):
         assert lib.slam_icp_set_schedule_wide(0, 1) == 0
         # the angle pre-tier: the turning pairs on the wide tier from their
         # initial transforms, beside phase 1 of the rest (with gangs, with heads only)
-        for amax, athr, gangs in ((24, 0.3, 24), (64, 0.05, 24), (8, 0.3, 0)):
+        # (kind 0: wide workgroups; 2 / 3: bulk gangs of that many workgroups)
+        for amax, athr, gangs, kind in ((24, 0.3, 24, 0), (64, 0.05, 24, 0), (8, 0.3, 0, 0), (48, 0.3, 24, 3),
+                                        (96, 0.05, 0, 2), (200, 0.05, 24, 3)):
             assert lib.slam_icp_set_schedule_gangs(gangs, 4) == 0
             assert lib.slam_icp_set_angle_tier(amax, athr) == 0
-            runs[("angle", amax, athr, gangs)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100,
-                                                             history=True)
+            assert lib.slam_icp_set_angle_tier_kind(kind) == 0
+            runs[("angle", amax, athr, gangs, kind)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05,
+                                                                   max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() == 0
         assert lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE) == 0
+        assert lib.slam_icp_set_angle_tier_kind(0) == 0
         # bulk gangs: both phases' bulk as gangs of 2 / 3 ordinary workgroups
         for parts in (2, 3):
             assert lib.slam_icp_set_bulk_gangs(4096, parts) == 0
@@ -499,12 +503,14 @@ def test_gang_timeouts_are_repaired(k):
         assert lib.slam_icp_set_schedule(-1, 1024) == 0
         assert lib.slam_icp_set_gang_wait(1) == 0
         lib.slam_icp_gang_timeouts()   # clear
-        for gangs, parts, wide, bulk, angle in ((64, 4, 0, 0, 0), (16, 0, 0, 0, 0), (0, 4, 16, 0, 0), (8, 4, 0, 2, 0),
-                                                (0, 4, 0, 3, 0), (0, 4, 0, 0, 16)):
+        for gangs, parts, wide, bulk, angle, kind in ((64, 4, 0, 0, 0, 0), (16, 0, 0, 0, 0, 0), (0, 4, 16, 0, 0, 0),
+                                                      (8, 4, 0, 2, 0, 0), (0, 4, 0, 3, 0, 0), (0, 4, 0, 0, 16, 0),
+                                                      (24, 4, 0, 0, 48, 3)):
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
             assert lib.slam_icp_set_schedule_wide(wide, 1) == 0
             assert lib.slam_icp_set_bulk_gangs(4096 if bulk else 0, max(bulk, 2)) == 0
             assert lib.slam_icp_set_angle_tier(angle, 0.1) == 0
+            assert lib.slam_icp_set_angle_tier_kind(kind) == 0
             r = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() > 0, (gangs, parts, wide)
             assert np.array_equal(r.iters, single.iters), (gangs, parts)
@@ -519,14 +525,14 @@ def test_gang_timeouts_are_repaired(k):
     assert lib.slam_icp_gang_timeouts() == 0
 
 
-@pytest.mark.parametrize("B", [5000, 4096, 1250, 37])
+@pytest.mark.parametrize("B", [9000, 5000, 4096, 1250, 37])
 def test_scheduler_order_is_a_stable_sort(B):
     """Phase 2's visiting order is the scheduler's stable bucket sort: the same
     permutation every run, unfinished pairs by bucket of log2 |dE| (largest
     |dE| first, 8 buckets per octave), pair index ascending inside a bucket,
     finished and out-of-bounds pairs last in index order, pairs that never
     started (out_iters 0: a timed-out phase-1 gang; key never written) first.
-    B > 4,096: the three-kernel sort; B <= 4,096: the one-workgroup sort of
+    B > 8,192: the three-kernel sort; B <= 8,192: the one-workgroup sort of
     the strong-scaling shards."""
     import ctypes
     import torch

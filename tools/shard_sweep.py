@@ -1,7 +1,7 @@
 """Strong-scaling projection on ONE GPU, done the way bench.py shards: every
 rank's shard of the ONE 10k C3 stream (slamhip.dist.shard_range over N ranks,
 N = 2, 4, 8) timed on its own (HIP events, median of 5 launches), under each
-scheduler setting "heads,gangs,parts,wide,share[,probe[,sort_one[,tier_limit[,xcd_map[,angle_max[,angle_centirad]]]]]]".  The
+scheduler setting "heads,gangs,parts,wide,share[,probe[,sort_one[,tier_limit[,xcd_map[,angle_max[,angle_centirad[,angle_kind]]]]]]]".  The
 projected N-GPU time is the slowest shard (bench.py takes the max over ranks).
 (bench.py --pairs P builds ANOTHER stream of P pairs: synthetic.make_sequence
 draws its noise after the whole trajectory, so a shorter stream is not a
@@ -69,6 +69,7 @@ def main():
             assert lib.slam_icp_set_xcd_map(v[8] if len(v) > 8 else -1) == 0
             if st != "auto":
                 assert lib.slam_icp_set_angle_tier(v[9] if len(v) > 9 else 0, (v[10] if len(v) > 10 else 30) / 100.0) == 0
+                assert lib.slam_icp_set_angle_tier_kind(v[11] if len(v) > 11 else 0) == 0
             line = []
             t1 = None
             for n in [1] + ranks:

@@ -74,9 +74,6 @@ SIGNATURES = {
     "slam_gn_iteration_schur_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                             c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                             c_ptr, c_ptr]),
-    "slam_gn_iterations_schur_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
-                                             c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
-                                             c_ptr, c_int, c_ptr]),
 }
 
 

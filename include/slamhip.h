@@ -218,23 +218,6 @@ int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea,
                                 double* pwork, double* work,
                                 double* out_chi2, int32_t* status,
                                 void* stream);
-/* `iterations` calls of slam_gn_iteration_schur_f64 in one: out_chi2[k] (k <
- * iterations) = chi2 before step k.  Every step but the last is added to the
- * poses by the next iteration's linearisation instead of an update launch of
- * its own (one dependent launch fewer per iteration, the same bits).  The
- * poses are final when the stream reaches the end of the call. */
-int slam_gn_iterations_schur_f64(double* poses, int32_t N, const int32_t* ea,
-                                 const int32_t* eb, const double* tf,
-                                 const double* w, int32_t E,
-                                 const int32_t* node_col,
-                                 const int32_t* slot_rc,
-                                 const int32_t* slot_ptr,
-                                 const int32_t* slot_items, int32_t n_slots,
-                                 int32_t nv, int32_t W, int32_t nv_band,
-                                 const int32_t* pslot, int32_t n_pslot,
-                                 double* pwork, double* work,
-                                 double* out_chi2, int32_t* status,
-                                 int32_t iterations, void* stream);
 
 /* ---- occupancy grid (src/produce_occupancy_grid.py) ------------------------
  * pts: packed (x, y) scan points, scan_off (S+1), pose4 (S x 4: cos theta,

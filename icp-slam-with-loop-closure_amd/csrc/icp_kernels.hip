@@ -42,10 +42,11 @@ __device__ int g_icp_status;                // nonzero: some pair was outside it
 // two reduction slabs of 16 doubles per wave at the front of the dynamic LDS
 // (block_sum_exact16, alternating between iterations), then 16 doubles of
 // per-pair constants (kept in LDS, not in registers across the NN search)
-constexpr int kPairConsts = 34;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab (16 sums + the
-                                  // arrival flag; an even count keeps the candidates 16-byte aligned)
+constexpr int kPairConsts = 42;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab (16 sums + the
+                                  // arrival flag), then kKab: the update wave 0 hands to the others (an even count keeps
+                                  // the candidates 16-byte aligned)
 __host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 16 + kPairConsts; }
-enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kPh0, kPhS, kBcast = 16 };
+enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kPh0, kPhS, kBcast = 16, kKab = 34 };
 
 struct IcpArgs {
     const double2* pts;
@@ -1301,43 +1302,76 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                                             parts, it, a.gang_wait, pconst + kBcast))
                 return;
         }
-        const double n = static_cast<double>(n1);
-        const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
-        const double mvy = (readlane_d(tot, 2) + readlane_d(tot, 3)) / n;
-        const double err = readlane_d(tot, 4) + readlane_d(tot, 5);
-        const double2 dp = *reinterpret_cast<const double2*>(pconst + kDpX);
-        const double2 mup = *reinterpret_cast<const double2*>(pconst + kMupX);
-        const double mux = fma(T.m02, 1.0, fma(T.m01, mup.y, T.m00 * mup.x));   // pc1_avg = T mu_p
-        const double muy = fma(T.m12, 1.0, fma(T.m11, mup.y, T.m10 * mup.x));
-        // S_p = sum (p - mu_p)(m - pc2_avg)^T, then S = X @ Y.T = R_T S_p
-        const double p00 = fma(-dp.x, mvx, readlane_d(tot, 6) + readlane_d(tot, 7));
-        const double p01 = fma(-dp.x, mvy, readlane_d(tot, 8) + readlane_d(tot, 9));
-        const double p10 = fma(-dp.y, mvx, readlane_d(tot, 10) + readlane_d(tot, 11));
-        const double p11 = fma(-dp.y, mvy, readlane_d(tot, 12) + readlane_d(tot, 13));
-        double s[4];
-        s[0] = fma(T.m01, p10, T.m00 * p00);
-        s[1] = fma(T.m01, p11, T.m00 * p01);
-        s[2] = fma(T.m11, p10, T.m10 * p00);
-        s[3] = fma(T.m11, p11, T.m10 * p01);
+        // The update is the same for every wave: wave 0 computes it and hands the
+        // new transform and the error to the others through LDS (one barrier;
+        // the same bits), so the other waves' SIMD issue slots go to the search
+        // (-DSLAM_KABSCH_ALL: every wave computes it, as before round 5)
+        SE2 Tn;
+        double err;
+#ifndef SLAM_KABSCH_ALL
+        if (wave == 0) {
+#else
+        {
+#endif
+            const double n = static_cast<double>(n1);
+            const double mvx = (readlane_d(tot, 0) + readlane_d(tot, 1)) / n;   // pc2_avg
+            const double mvy = (readlane_d(tot, 2) + readlane_d(tot, 3)) / n;
+            err = readlane_d(tot, 4) + readlane_d(tot, 5);
+            const double2 dp = *reinterpret_cast<const double2*>(pconst + kDpX);
+            const double2 mup = *reinterpret_cast<const double2*>(pconst + kMupX);
+            const double mux = fma(T.m02, 1.0, fma(T.m01, mup.y, T.m00 * mup.x));   // pc1_avg = T mu_p
+            const double muy = fma(T.m12, 1.0, fma(T.m11, mup.y, T.m10 * mup.x));
+            // S_p = sum (p - mu_p)(m - pc2_avg)^T, then S = X @ Y.T = R_T S_p
+            const double p00 = fma(-dp.x, mvx, readlane_d(tot, 6) + readlane_d(tot, 7));
+            const double p01 = fma(-dp.x, mvy, readlane_d(tot, 8) + readlane_d(tot, 9));
+            const double p10 = fma(-dp.y, mvx, readlane_d(tot, 10) + readlane_d(tot, 11));
+            const double p11 = fma(-dp.y, mvy, readlane_d(tot, 12) + readlane_d(tot, 13));
+            double s[4];
+            s[0] = fma(T.m01, p10, T.m00 * p00);
+            s[1] = fma(T.m01, p11, T.m00 * p01);
+            s[2] = fma(T.m11, p10, T.m10 * p00);
+            s[3] = fma(T.m11, p11, T.m10 * p01);
 
-        // ---- closed-form 2x2 Kabsch: R maximising tr(R S) ---------------------
-        // Equals V diag(1, det(V U^T)) U^T of the reference's SVD route.
-        const double cs = s[0] + s[3];
-        const double sn = s[1] - s[2];
-        const double r = sqrt(cs * cs + sn * sn);
-        const double c = r > 0.0 ? cs / r : 1.0;
-        const double si = r > 0.0 ? sn / r : 0.0;
-        // t = pc2_avg - R @ pc1_avg (dgemv order)
-        double tx = mvx - fma(-si, muy, c * mux);
-        double ty = mvy - fma(c, muy, si * mux);
-        if (a.rotation_only) {   // src/icp.py:65-66
-            tx = 0.0;
-            ty = 0.0;
+            // ---- closed-form 2x2 Kabsch: R maximising tr(R S) ---------------------
+            // Equals V diag(1, det(V U^T)) U^T of the reference's SVD route.
+            const double cs = s[0] + s[3];
+            const double sn = s[1] - s[2];
+            const double r = sqrt(cs * cs + sn * sn);
+            const double c = r > 0.0 ? cs / r : 1.0;
+            const double si = r > 0.0 ? sn / r : 0.0;
+            // t = pc2_avg - R @ pc1_avg (dgemv order)
+            double tx = mvx - fma(-si, muy, c * mux);
+            double ty = mvy - fma(c, muy, si * mux);
+            if (a.rotation_only) {   // src/icp.py:65-66
+                tx = 0.0;
+                ty = 0.0;
+            }
+            SE2 D;
+            D.m00 = c;  D.m01 = -si; D.m02 = tx;
+            D.m10 = si; D.m11 = c;   D.m12 = ty;
+            Tn = se2_mul(D, T);   // src/icp.py:67
+#ifndef SLAM_KABSCH_ALL
+            if (lane == 0) {
+                pconst[kKab + 0] = Tn.m00;
+                pconst[kKab + 1] = Tn.m01;
+                pconst[kKab + 2] = Tn.m02;
+                pconst[kKab + 3] = Tn.m10;
+                pconst[kKab + 4] = Tn.m11;
+                pconst[kKab + 5] = Tn.m12;
+                pconst[kKab + 6] = err;
+            }
+#endif
         }
-        SE2 D;
-        D.m00 = c;  D.m01 = -si; D.m02 = tx;
-        D.m10 = si; D.m11 = c;   D.m12 = ty;
-        const SE2 Tn = se2_mul(D, T);   // src/icp.py:67
+#ifndef SLAM_KABSCH_ALL
+        __syncthreads();
+        Tn.m00 = pconst[kKab + 0];
+        Tn.m01 = pconst[kKab + 1];
+        Tn.m02 = pconst[kKab + 2];
+        Tn.m10 = pconst[kKab + 3];
+        Tn.m11 = pconst[kKab + 4];
+        Tn.m12 = pconst[kKab + 5];
+        err = pconst[kKab + 6];
+#endif
 
         stamp(3);
         if constexpr (STEP) {

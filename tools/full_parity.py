@@ -1,6 +1,6 @@
 """Parity of the benchmarked path over EVERY pair of the C3 stream: the GPU's
-batched ICP (default scheduler; the full 10k batch and the shards ranks 0 get
-at 2 / 4 / 8 GPUs, which run the gang / CU-exclusive head tiers) against the
+batched ICP (default scheduler; the full 10k batch and EVERY rank's shard at
+2 / 4 / 8 GPUs, which run the angle pre-tier and the exchange / head tiers) against the
 CPU oracle (oracle/icp_oracle.py, vectorised NumPy, bit-exact with
 src/icp.py), run on the host cores with joblib.  GPU only; ~2 minutes on 16
 cores.
@@ -56,13 +56,13 @@ def main():
     seq = synthetic.make_sequence(n + 1, seed=2025)
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, n + 1)])
     ss = k.ScanSet(seq.scans)
-    runs = {}
-    for shard in (n, n // 2, n // 4, n // 8):
-        runs[shard] = k.icp_batch(ss, np.arange(1, shard + 1), np.arange(0, shard), inits[:shard],
-                                  epsilon=EPS, max_iters=MAX_ITERS)
-    for shard in (n // 2, n // 4, n // 8):   # the last shard of each world size as well
-        runs[f"last_{shard}"] = (n - shard, k.icp_batch(ss, np.arange(n - shard + 1, n + 1), np.arange(n - shard, n),
-                                                         inits[n - shard:], epsilon=EPS, max_iters=MAX_ITERS))
+    from slamhip import dist as sd
+    runs = {"all": (0, k.icp_batch(ss, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=EPS, max_iters=MAX_ITERS))}
+    for nr in (2, 4, 8):   # EVERY rank's shard (the tier profile depends on the shard size)
+        for r in range(nr):
+            lo, hi, _ = sd.shard_range(n, nr, r)
+            runs[f"ranks{nr}_rank{r}"] = (lo, k.icp_batch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi],
+                                                           epsilon=EPS, max_iters=MAX_ITERS))
     from joblib import Parallel, delayed
     t0 = time.perf_counter()
     ref = Parallel(n_jobs=workers, backend="loky", batch_size=16)(
@@ -76,19 +76,17 @@ def main():
     out = {"workload": f"C3 stream seed 2025, {n} consecutive pairs of 1081-point scans, scripts/main.py parameters",
            "oracle": "oracle/icp_oracle.py (vectorised, bit-exact with the reference's src/icp.py)",
            "oracle_seconds": round(dt, 1), "oracle_workers": workers, "runs": {}}
-    for key, val in runs.items():
-        lo, res = (0, val) if isinstance(key, int) else val
+    for key, (lo, res) in runs.items():
         cnt = len(res.iters)
         sl = slice(lo, lo + cnt)
         dtf = np.abs(res.tf - rtf[sl]).max(axis=(1, 2))
         derr = np.abs(res.err - rerr[sl]) / np.maximum(1.0, np.abs(rerr[sl]))
-        name = f"first_{key}_pairs" if isinstance(key, int) else f"last_{key[5:]}_pairs"
-        out["runs"][name] = {
+        out["runs"][key] = {
             "pairs": cnt, "first_pair": lo, "iters_equal": int(np.sum(res.iters == rit[sl])),
             "max_abs_tf_diff": float(dtf.max()), "max_rel_err_diff": float(derr.max()),
             "pairs_over_1e-9": int(np.sum((dtf > 1e-9) | (derr > 1e-9) | (res.iters != rit[sl]))),
             "longest_pair_iters": int(res.iters.max())}
-    full = runs[n]
+    full = runs["all"][1]
     aerr = np.abs(full.err - rerr)
     margin = np.minimum(m_eps, m_d)
     ratio = margin / np.maximum(aerr, 1e-300)

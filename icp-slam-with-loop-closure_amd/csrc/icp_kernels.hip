@@ -280,6 +280,13 @@ struct MinI { __device__ int operator()(int a, int b) const { return min(a, b); 
 struct MaxI { __device__ int operator()(int a, int b) const { return max(a, b); } };
 struct MinU { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return min(a, b); } };
 struct MaxU { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); } };
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// two independent 16-bit maxima in one word (v_pk_max_u16)
+struct MaxPk16 {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+    }
+};
 // every lane returns the wave's min / max (no NaN inputs)
 __device__ __forceinline__ float wave_min_f(float v) { return ord2f(wave_reduce_i<int>(f2ord(v), MinI())); }
 __device__ __forceinline__ float wave_max_f(float v) { return ord2f(wave_reduce_i<int>(f2ord(v), MaxI())); }
@@ -519,6 +526,17 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
         const float by0 = wave_min_f(act[k] ? qy[k] : INFINITY);
         const float by1 = wave_max_f(act[k] ? qy[k] : -INFINITY);
         const float gM2 = wave_max_nn(act[k] ? M2[k] : 0.0f);
+#ifndef SLAM_NO_WINX
+        // sub-chunks inside EVERY active lane's window ([wlo, whi): the windows'
+        // intersection) are needed by no active lane and bound nothing it needs
+        // (the clearance covers the candidates outside its own window): not live
+        const uint32_t wx = wave_reduce_i<uint32_t>(
+            act[k] ? (static_cast<uint32_t>(ws[k]) << 16) | static_cast<uint32_t>(0xffff - (ws[k] + kWin)) : 0u,
+            MaxPk16());
+        const int wlo = static_cast<int>(wx >> 16), whi = 0xffff - static_cast<int>(wx & 0xffff);
+#else
+        const int wlo = 0, whi = 0;
+#endif
         float gf = INFINITY, lmin = INFINITY;
         flap(5);
         for (int w = 0; w < nw; ++w) {
@@ -527,7 +545,7 @@ __device__ __forceinline__ void nn_window_pruned(const float2* __restrict__ cand
             const float glb = box_lb(f32x2{bx0, by0}, f32x2{bx1, by1}, box8[min(sl, nsub - 1)]);
             const bool gl = glb <= gM2;
             gf = (sl < nsub && !gl) ? fminf(gf, glb) : gf;
-            uint64_t live = __ballot((sl < nsub) & gl);
+            uint64_t live = __ballot((sl < nsub) & gl & ((sl < wlo) | (sl >= whi)));
             if (stamping) {
                 tsub[3] += __popcll(live);
                 g_live += __popcll(live);

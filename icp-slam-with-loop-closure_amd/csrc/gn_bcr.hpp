@@ -9,6 +9,7 @@
 
 namespace slamhip {
 
+
 // workspace carve-up of the explicit-inverse path (nb = ceil(nv / Wb) blocks)
 struct BcrGjBufs {
     double *D, *E0, *E1, *Xs, *Ys, *SP, *SN;   // nb x Wb x Wb each
@@ -35,6 +36,10 @@ struct BcrSchur {
     double* xb;             // nbd: the border's solution
     int32_t* status;        // the iteration's status word (a fused wait that timed out sets 2)
 };
+// The XCD-local fused back-substitution on (1, default) or off (0).
+void bcr_gj_set_fused(int on);
+int bcr_gj_get_fused();
+void bcr_gj_set_fused_wait(uint32_t ticks);   // diagnostics: the longest wait (s_memrealtime ticks)
 BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc);
 int64_t bcr_gj_work_size(int32_t nv, int32_t Wb, int32_t mc);
 int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_t* status, hipStream_t st,

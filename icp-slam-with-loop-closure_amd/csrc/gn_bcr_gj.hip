@@ -913,6 +913,7 @@ __global__ __launch_bounds__(kThreads) void back_schur_xcd_kernel(const double* 
     __shared__ uint32_t xh[2][2 * WB];   // the neighbours' x as 32-bit halves (lo, hi)
     const int tid = threadIdx.x;
     if (blockIdx.x & 7) return;   // (uniform) not on the working XCD
+
     int w = static_cast<int>(blockIdx.x >> 3);
     int s = 1;
     while (2 * s < nb) s *= 2;   // the top level
@@ -1307,26 +1308,35 @@ int bcr_border_solve(const double* Z, const double* BR, const double* rhs, const
     return check_launch("gn border solve");
 }
 
+static int g_fused = [] {   // default on; SLAMHIP_GN_FUSED_BACK=0 turns it off
+    const char* e = getenv("SLAMHIP_GN_FUSED_BACK");
+    return e && e[0] == '0' ? 0 : 1;
+}();
+static uint32_t g_fused_wait = 20000000;   // 0.2 s of s_memrealtime ticks per wait
+void bcr_gj_set_fused(int on) { g_fused = on ? 1 : 0; }
+int bcr_gj_get_fused() { return g_fused; }
+void bcr_gj_set_fused_wait(uint32_t ticks) { g_fused_wait = ticks; }
+
 int bcr_gj_back(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, hipStream_t st, const BcrSchur* sc) {
     const int nb = (nv + Wb - 1) / Wb;
-    // off by default: the XCD-local tagged hand-offs gain 1.5 % at C4
-    // (profiles/r05_gn_ab_xcdback.txt: 5,455-5,463 against 5,370-5,392 it/s)
-    // and rest on the round-robin workgroup -> XCD dispatch (a violated
-    // assumption times out: status 2, an error, never a wrong answer); the
-    // first form (flags with agent-scope release / acquire across XCDs) was
-    // slower than the launches (2,926-2,949 it/s, profiles/r05_gn_ab_schur.txt)
-    static const bool fused = [] {
-        const char* e = getenv("SLAMHIP_GN_FUSED_BACK");
-        return e && e[0] == '1';
-    }();
-    if (sc && fused && nb > 1) {   // every level in one launch on one XCD (tagged granules)
+    // the XCD-local tagged hand-offs (every level in one launch; default since
+    // round 5: 5,418-5,453 it/s against 5,385-5,388 with a launch per level,
+    // profiles/r05_gn_ab_fused2.txt; the pose update fused into it as well was
+    // slower, 5,244-5,306: each workgroup's scattered pose read-modify-write
+    // holds its slot longer and delays the finer levels' dispatch); they rest
+    // on the round-robin workgroup -> XCD dispatch: a violated
+    // assumption times out (status 2; slamhip.gn re-runs the step with
+    // bcr_gj_set_fused(0)), never a hang or a silent wrong answer.  The first
+    // form (flags with agent-scope release / acquire across XCDs) was slower
+    // than the launches (2,926-2,949 it/s, profiles/r05_gn_ab_schur.txt)
+    if (sc && g_fused && nb > 1) {   // every level in one launch on one XCD (tagged granules)
         using BackXFn = void (*)(const double*, const double*, const double*, double*, const double*, int32_t, int32_t,
                                  int32_t, uint64_t*, uint32_t, int32_t*);
         static const BackXFn backxs[6] = {bcrgj::back_schur_xcd_kernel<1>, bcrgj::back_schur_xcd_kernel<2>,
                                           bcrgj::back_schur_xcd_kernel<3>, bcrgj::back_schur_xcd_kernel<4>,
                                           bcrgj::back_schur_xcd_kernel<5>, bcrgj::back_schur_xcd_kernel<6>};
         hipLaunchKernelGGL(backxs[Wb / 16 - 1], dim3(8 * (nb - 1)), dim3(bcrgj::kThreads), 0, st, b.Xs, b.Ys, b.bzo,
-                           b.x, sc->xb, sc->nbd, nb, mc, b.xg, static_cast<uint32_t>(20000000), sc->status);
+                           b.x, sc->xb, sc->nbd, nb, mc, b.xg, g_fused_wait, sc->status);
         return check_launch("gn bcr (explicit inverse, Schur border) XCD-local back-substitution");
     }
     if (sc) {   // one column: z_i[:, 0] - z_i[:, B] x_b

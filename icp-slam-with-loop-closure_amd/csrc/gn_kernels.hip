@@ -48,6 +48,7 @@ __device__ __forceinline__ double wrap_pi(double a) {
     return a - 2.0 * M_PI * floor((a + M_PI) / (2.0 * M_PI));
 }
 
+
 // n doubles at z <- 0 by grid-stride double2 stores (a head / tail double by
 // thread 0 when z is not 16-byte aligned or the count is odd)
 __device__ __forceinline__ void zero_doubles(double* __restrict__ z, int64_t n, int64_t t, int64_t stride) {
@@ -731,6 +732,21 @@ int slam_gn_set_solver(int mode) {
 }
 
 int slam_gn_get_solver(void) { return g_gn_solver; }
+
+// The Schur path's back-substitution as ONE XCD-local launch (1, default) or
+// one launch per level (0); slamhip.gn falls back to 0 for the rest of the
+// process when a fused wait timed out (status bit 2).
+int slam_gn_set_fused_back(int on) {
+    bcr_gj_set_fused(on);
+    return ok();
+}
+int slam_gn_get_fused_back(void) { return bcr_gj_get_fused(); }
+// Diagnostics: the fused back-substitution's longest wait (s_memrealtime
+// ticks, 0: the default 0.2 s) — a tiny wait forces the timeout path.
+int slam_gn_set_fused_wait(uint32_t ticks) {
+    bcr_gj_set_fused_wait(ticks ? ticks : 20000000u);
+    return ok();
+}
 
 static int64_t window_dim(int32_t W) {
     int64_t MP = 32;

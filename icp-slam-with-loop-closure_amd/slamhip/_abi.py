@@ -74,6 +74,9 @@ SIGNATURES = {
     "slam_gn_iteration_schur_f64": (c_int, [c_ptr, c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                             c_ptr, c_int, c_int, c_int, c_int, c_ptr, c_int, c_ptr, c_ptr, c_ptr,
                                             c_ptr, c_ptr]),
+    "slam_gn_set_fused_back": (c_int, [c_int]),
+    "slam_gn_get_fused_back": (c_int, []),
+    "slam_gn_set_fused_wait": (c_int, [ctypes.c_uint32]),
 }
 
 

@@ -332,6 +332,7 @@ class GaussNewton:
         if p.pslot is not None:   # the Schur-accumulating bordered path
             mc = 16 * ((p.nv - p.nv_band + 16) // 16)
             self.pslot = dv.to_dev(p.pslot, np.int32, dev)
+
             self.pwork = dv.empty((max(len(p.schur_blocks), 1) * mc * mc,), np.float64, dev)
         self.chi2 = None
         self._eager_done = False
@@ -389,6 +390,11 @@ class GaussNewton:
     def _run(self, iterations, stream, graph):
         t = dv.torch()
         self.status.zero_()   # a failed earlier run must not poison this one
+        lib = _abi.lib()
+        # the fused back-substitution rests on the round-robin XCD dispatch; if a
+        # wait times out (status bit 2) the steps are re-run without it
+        fused = self.plan.pslot is not None and self.plan.nv_band < self.plan.nv and lib.slam_gn_get_fused_back()
+        backup = self.poses.clone() if fused else None
         if graph is None:
             graph = self._eager_done and stream is None and iterations > 0
         if graph:
@@ -409,9 +415,16 @@ class GaussNewton:
             self._eager_done = True
         out = chis[:iterations].cpu().numpy().copy()
         st = int(self.status.cpu().numpy()[0])
+        if st & 2 and backup is not None:
+            import warnings
+            warnings.warn("Gauss-Newton: the XCD-local back-substitution timed out (workgroup dispatch not "
+                          "round-robin over the XCDs?); re-running with one launch per level", RuntimeWarning)
+            lib.slam_gn_set_fused_back(0)
+            self._graphs.clear()
+            self.poses.copy_(backup)
+            return self._run(iterations, stream, graph)
         if st & 2:
-            raise _abi.SlamHipError("Gauss-Newton: the fused back-substitution timed out waiting for a block "
-                                    "(unset SLAMHIP_GN_FUSED_BACK: the per-level launches)")
+            raise _abi.SlamHipError("Gauss-Newton: the fused back-substitution timed out waiting for a block")
         if st != 0:
             raise _abi.SlamHipError("Gauss-Newton: H is not positive definite (disconnected graph?)")
         self.chi2 = out

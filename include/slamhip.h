@@ -205,6 +205,10 @@ int slam_gn_iteration_bordered_f64(double* poses, int32_t N, const int32_t* ea,
  * the top block forms S and x_b = S^-1 s, and the back-substitution runs on
  * one column.  Same result as slam_gn_iteration_bordered_f64 to rounding;
  * needs the explicit-inverse cyclic reduction (SLAM_EINVAL otherwise).
+ * The back-substitution runs as ONE XCD-local launch by default
+ * (slam_gn_set_fused_back): a fused wait that timed out sets *status |= 2,
+ * the step is then invalid and is re-run with slam_gn_set_fused_back(0)
+ * (slamhip.gn does this).
  * work: slam_gn_work_size_bordered(N, E, W, nv - nv_band) doubles. */
 int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea,
                                 const int32_t* eb, const double* tf,
@@ -218,6 +222,13 @@ int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea,
                                 double* pwork, double* work,
                                 double* out_chi2, int32_t* status,
                                 void* stream);
+/* The Schur path's back-substitution: one XCD-local launch (1, default) or
+ * one launch per level (0). */
+int slam_gn_set_fused_back(int on);
+int slam_gn_get_fused_back(void);
+/* Diagnostics: the fused back-substitution's longest wait in s_memrealtime
+ * ticks (0: the default 0.2 s); a tiny wait forces the timeout path. */
+int slam_gn_set_fused_wait(uint32_t ticks);
 
 /* ---- occupancy grid (src/produce_occupancy_grid.py) ------------------------
  * pts: packed (x, y) scan points, scan_off (S+1), pose4 (S x 4: cos theta,

@@ -281,6 +281,40 @@ def test_gn_graph_replay_matches_eager():
     assert np.array_equal(a.host_poses(), b.host_poses())
 
 
+@pytest.mark.gpu
+def test_gn_fused_back_substitution_and_fallback():
+    """The Schur path's XCD-local back-substitution (every level in one launch,
+    tagged hand-offs; default) equals the per-level launches bit for bit (C4,
+    6 iterations, eager and graph-replayed); with its wait forced down to one
+    tick every fused step times out, GaussNewton warns, restores the poses and
+    re-runs with the per-level launches: the same bits again."""
+    import warnings
+    from slamhip import _abi, gn, synthetic
+    lib = _abi.lib()
+    guess, ea, eb, tf, truth = synthetic.lap_graph_c4()
+    try:
+        assert lib.slam_gn_set_fused_back(0) == 0
+        a = gn.GaussNewton(guess, ea, eb, tf)
+        chi_a = np.concatenate([a.run(1, graph=False), a.run(5, graph=True)])
+        assert lib.slam_gn_set_fused_back(1) == 0 and lib.slam_gn_get_fused_back() == 1
+        b = gn.GaussNewton(guess, ea, eb, tf)
+        chi_b = np.concatenate([b.run(1, graph=False), b.run(5, graph=True)])
+        assert np.array_equal(chi_a, chi_b)
+        assert np.array_equal(a.host_poses(), b.host_poses())
+        assert lib.slam_gn_set_fused_wait(1) == 0
+        c = gn.GaussNewton(guess, ea, eb, tf)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            chi_c = np.concatenate([c.run(1, graph=False), c.run(5, graph=False)])
+        assert any("timed out" in str(x.message) for x in w)
+        assert lib.slam_gn_get_fused_back() == 0
+        assert np.array_equal(chi_a, chi_c)
+        assert np.array_equal(a.host_poses(), c.host_poses())
+    finally:
+        lib.slam_gn_set_fused_wait(0)
+        lib.slam_gn_set_fused_back(1)
+
+
 def test_oracle_jacobians_match_finite_differences():
     """The GN oracle's analytic Jacobians A = de/dx_a, B = de/dx_b against
     central differences of its own residual (self-consistency of the oracle)."""

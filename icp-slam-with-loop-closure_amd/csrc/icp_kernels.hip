@@ -344,7 +344,8 @@ constexpr int kSub = 8;
 #define SLAM_KWIN 4
 #endif
 #ifndef SLAM_KBATCH
-#define SLAM_KBATCH 3
+#define SLAM_KBATCH 4   // round 5, after the windows' intersection left the live sets: 4 for 3 (10k bench
+                        // 4.00-4.03 ms against 4.06-4.07; 2: 4.21-4.23, 5 / 6: 4.07; profiles/r05_ab_kbatch*.txt)
 #endif
 constexpr int kWin = SLAM_KWIN;  // window sub-chunks (32 candidates); 2/5/6/8 measured slower
 constexpr int kStageUnroll = 4;  // staging loads in flight per thread

@@ -3023,11 +3023,15 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     }
     int rc = 0;
     SideStream* side0 = nullptr;
+    // the stream the phases run on: the caller's, or with the pre-tier stream3
+    // (the pre-tier then runs on the caller's stream right behind the angle
+    // sort, so its workgroups are dispatched before phase 1's, which waits for
+    // an event; joined back before the repair launches)
+    hipStream_t ms = s;
     if (ap) {
         // the turning pairs first in order0 (their out_iters set to 0: not
-        // started), then the wide tier for them from their initial transforms on
-        // stream3, launched before phase 1 so that its workgroups reach the CUs
-        // first; phase 1 runs the rest (order0 from *ap_k on)
+        // started), then their tier from their initial transforms; phase 1
+        // runs the rest (order0 from *ap_k on)
         int dev = 0;
         if (hipGetDevice(&dev) == hipSuccess) side0 = side_stream(dev);
         if (!side0) return (void)hipFreeAsync(ws, s), fail(SLAM_EHIP, "icp scheduler: side streams");
@@ -3037,12 +3041,14 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                            args.out_iters);
         if (hipEventRecord(side0->fork, s) != hipSuccess || hipStreamWaitEvent(side0->stream3, side0->fork, 0) != hipSuccess)
             rc = fail(SLAM_EHIP, "icp scheduler: fork");
+        else
+            ms = side0->stream3;
         IcpArgs w = args;
         w.order = order0;
         w.take_lt = ap_k;
         if (rc == 0)
-            rc = apg ? launch_bulk_gangs(w, ap, apg, max_n2, side0->stream3, ap_slots)
-                     : launch_wide(w, ap, max_n1, max_n2, side0->stream3, ap_slots, ap_cand, cfg_share);
+            rc = apg ? launch_bulk_gangs(w, ap, apg, max_n2, s, ap_slots)
+                     : launch_wide(w, ap, max_n1, max_n2, s, ap_slots, ap_cand, cfg_share);
         a.order = order0;
         a.skip_lt = ap_k;
     }
@@ -3054,7 +3060,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
         rc = launch_bulk_gangs(a, B, bg, max_n2, s, bulk_slots);
     } else {
-        rc = launch(false, a, B, max_n1, max_n2, stream);
+        rc = launch(false, a, B, max_n1, max_n2, ms);
     }
     if (rc == 0) {
         const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
@@ -3063,15 +3069,15 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         if (bg) (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
         if (B <= kSortOneMax && g_sched_sort_one) {
             // one launch on the phase boundary: the sort, and the exchange slots zeroed beside it
-            hipLaunchKernelGGL(sched_sort_one_kernel<0>, dim3(1), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
+            hipLaunchKernelGGL(sched_sort_one_kernel<0>, dim3(1), dim3(kSortBlock), 0, ms, args.out_iters, key, B, thr,
                                order, gang_slots, static_cast<int64_t>(G + Wd > 0 ? gang_slot_bytes / sizeof(uint64_t) : 0),
                                order0, ap_k, static_cast<const double*>(nullptr), 0, static_cast<int32_t*>(nullptr));
         } else {
-            if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, s);
-            hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, args.out_iters, key, B, thr,
+            if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, ms);
+            hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, ms, args.out_iters, key, B, thr,
                                hist, bucket);
-            hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
-            hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, s, bucket, B, hist, order);
+            hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, ms, hist, nblk);
+            hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, ms, bucket, B, hist, order);
         }
         rc = check_launch("icp scheduler kernels");
     }
@@ -3092,7 +3098,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             // the rest on the side stream behind the fork event, which resolves
             // after the first launches are queued; join before the workspace is freed
             const int H = hinst ? heads : GW;
-            if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess ||
+            if (hipEventRecord(side->fork, ms) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess ||
                 hipStreamWaitEvent(side->stream2, side->fork, 0) != hipSuccess ||
                 hipStreamWaitEvent(side->stream3, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
@@ -3101,7 +3107,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             if (rc == 0 && G > 0) {
                 IcpArgs g = a;
                 g.order = order + Wd;
-                rc = launch_gangs(g, G, parts, team, max_n1, max_n2, s, gang_slots + wide_slot_words);
+                rc = launch_gangs(g, G, parts, team, max_n1, max_n2, ms, gang_slots + wide_slot_words);
             }
             if (rc == 0 && H > GW) {
                 IcpArgs h = a;
@@ -3121,6 +3127,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                             hipStreamWaitEvent(s, side->join2, 0) != hipSuccess ||
                             hipStreamWaitEvent(s, side->join3, 0) != hipSuccess))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
+            // (with the pre-tier, stream3 = ms: join3 also joins the phases and the gangs)
             if (rc == 0 && (GW > 0 || bg)) {
                 // repair: a wide / gang pair whose partners did not all arrive
                 // stopped without writing, leaving it paused at the phase-1 state;
@@ -3136,11 +3143,13 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 rc = launch(false, r, ap, max_n1, max_n2, stream);
             }
         } else {
-            rc = launch(false, a, B, max_n1, max_n2, stream);
+            if (ms != s && (hipEventRecord(side0->join3, ms) != hipSuccess || hipStreamWaitEvent(s, side0->join3, 0) != hipSuccess))
+                rc = fail(SLAM_EHIP, "icp scheduler: wait");
+            if (rc == 0) rc = launch(false, a, B, max_n1, max_n2, stream);
         }
     }
-    if (ap && side0 && rc != 0) {   // an error after the pre-tier's fork: still join its stream before the free
-        (void)hipEventRecord(side0->join3, side0->stream3);
+    if (ms != s && rc != 0) {   // an error after the pre-tier's fork: still join the phase stream before the free
+        (void)hipEventRecord(side0->join3, ms);
         (void)hipStreamWaitEvent(s, side0->join3, 0);
     }
     (void)hipFreeAsync(ws, s);

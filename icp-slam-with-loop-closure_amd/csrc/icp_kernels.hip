@@ -2569,11 +2569,12 @@ static thread_local int g_angle_kind = 0;
 //        wide workgroups sharing a CU kAutoShare ways, no phase-2 tiers;
 //   B <= kSortOneMax (4- and 2-rank shards): the angle pre-tier as bulk gangs
 //        of 3 (kAutoMidAngle pairs) and, in phase 2, 64 heads, the first 24 as
-//        gangs of 4 (5,000 pairs: 2.76 ms against 3.77 with the heads alone);
+//        gangs of 4 (5,000 pairs: 2.55 ms with 96 pre-tier pairs, 2.79 with 48, 3.77
+//        with the heads alone; profiles/r05_shard_sweep11.txt);
 //   larger batches: no tiers.
 static thread_local int g_sched_auto = 1;
 constexpr int kAutoSmall = 2048;
-constexpr int kAutoMidAngle = 48;
+constexpr int kAutoMidAngle = 96;
 constexpr int kAutoAngle = SLAM_AUTO_ANGLE;
 constexpr int kAutoShare = SLAM_AUTO_SHARE;
 

@@ -108,7 +108,7 @@ struct IcpArgs {
     // belong to pairs another tier runs (NULL: none); an order entry < 0 is
     // padding (both: the workgroup leaves at once)
     const int32_t* skip_lt;
-    const int32_t* take_lt;   // wide tier: slots at or past *take_lt leave at once (NULL: none)
+    const int32_t* take_lt;   // the pre-tier's launch: slots at or past *take_lt leave at once (NULL: none)
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
 #ifndef SLAM_TAIL_SHARE
@@ -2551,10 +2551,11 @@ static thread_local int g_sched_warm = 0;
 // batches of <= kSortOneMax pairs sort on one workgroup (diagnostics: 0 = the
 // three-kernel sort at every size)
 static thread_local int g_sched_sort_one = 1;
-// Angle pre-tier (batches below the tier limit): up to g_angle_max pairs whose
-// initial transform turns by more than g_angle_thresh rad — the C3 stream's
-// long pairs all start at a turn of 0.5-3 rad — run on
-// the wide tier from the start, beside phase 1 of the others (0: off)
+// Angle pre-tier (batches of up to kSortOneMax pairs): up to g_angle_max pairs
+// whose initial transform turns by more than g_angle_thresh rad — the C3
+// stream's long pairs all start at a turn of 0.5-3 rad —
+// run on a tier of their own from the start, beside phase 1 of the others
+// (0: off)
 static thread_local int g_angle_max = 0;
 static thread_local float g_angle_thresh = 0.3f;
 // the pre-tier's kind: 0 the wide tier (g_wide_share workgroups per CU), or
@@ -2964,8 +2965,8 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const int wide_parts = (max_n1 + 63) / 64;
     const bool wide_ok = g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap && wide_parts <= kTeamMaxParts &&
                          wide_lds_bytes(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) <= kMaxLds;
-    // angle pre-tier: the turning pairs on the wide tier from the start (its
-    // stream, stream3, is then busy: no phase-2 wide tier)
+    // angle pre-tier: the turning pairs on their own tier from the start (with
+    // it, no phase-2 wide tier: measured slower, profiles/r05_shard_sweep8.txt)
     const BulkGangInstance* apg = cfg_akind >= 2 ? pick_bulk_gang_instance(max_n1, cfg_akind) : nullptr;
     const int ap = (cfg_angle > 0 && (cfg_akind >= 2 ? apg != nullptr : wide_ok) && B <= kSortOneMax &&
                     g_sched_sort_one && B >= g_bulk_gang_below)
@@ -3259,9 +3260,10 @@ int slam_icp_set_xcd_map(int run) {
     g_xcd_map = run < 0 ? 16 : run;
     return ok();
 }
-// Angle pre-tier (see launch_batch): batches below the tier limit run up to
+// Angle pre-tier (see launch_batch): batches of up to 8,192 pairs run up to
 // `max_pairs` pairs whose initial transform turns by more than `thresh_rad`
-// on the wide tier from the start (0: off).  Results are bit-identical.
+// on a tier of their own from the start (kind: slam_icp_set_angle_tier_kind;
+// 0: off).  Results are bit-identical.
 int slam_icp_set_angle_tier(int max_pairs, float thresh_rad) {
     if (max_pairs < 0 || max_pairs > 1024 || !(thresh_rad >= 0.0f))
         return fail(SLAM_EINVAL, "angle tier: %d pairs, threshold %g", max_pairs, static_cast<double>(thresh_rad));

@@ -313,25 +313,27 @@ int slam_icp_set_gang_wait(uint32_t ticks);
  * bucket sort (device arrays; order[] receives B pair indices). */
 int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float thresh, int32_t* order,
                         void* stream);
-/* Diagnostics: batches of <= 4,096 pairs sort at the phase boundary on one
+/* Diagnostics: batches of <= 8,192 pairs sort at the phase boundary on one
  * workgroup (1, default; slam_icp_sched_sort uses it at those sizes too) or
  * with the three-kernel sort (0).  The order is the same. */
 int slam_icp_set_sched_sort_one(int on);
 /* Diagnostics: batches of fewer than `pairs` pairs get the scheduler's tail
  * tiers (heads, gangs, wide); 0 restores the default (4,096). */
 int slam_icp_set_tier_limit(int pairs);
-/* Diagnostics: the angle pre-tier — batches below the tier limit run up to
+/* Diagnostics: the angle pre-tier — batches of up to 8,192 pairs run up to
  * `max_pairs` pairs whose initial transform turns by more than `thresh_rad`
- * on the wide tier from the start, beside the two-phase schedule of the
- * others (0: off).  Results are bit-identical. */
+ * on a tier of their own from the start (slam_icp_set_angle_tier_kind),
+ * beside the two-phase schedule of the others (0: off).  Results are
+ * bit-identical. */
 int slam_icp_set_angle_tier(int max_pairs, float thresh_rad);
-/* The scheduler's automatic tier profile by batch size (1, default: the angle
- * pre-tier below 2,048 pairs, heads + gangs below 4,096, none above; DESIGN.md
- * section 6) or the explicit settings (0).  Any of the tier setters above
- * selects the explicit settings; 1 restores their defaults too. */
 /* Diagnostics: the angle pre-tier's kind, 0 the wide tier, 2 / 3 bulk gangs
  * of that many ordinary workgroups per pair. */
 int slam_icp_set_angle_tier_kind(int kind);
+/* The scheduler's automatic tier profile by batch size (1, default; DESIGN.md
+ * section 6): below 2,048 pairs 24 pre-tier pairs on wide workgroups; 2,048 -
+ * 8,192 pairs 96 pre-tier pairs on gangs of 3 plus 64 phase-2 heads, the first
+ * 24 as gangs of 4; larger batches no tiers.  0: the explicit settings; any of
+ * the tier setters above selects them, 1 restores their defaults too. */
 int slam_icp_set_schedule_auto(int on);
 /* Diagnostics: the XCD-aware pair map of launches in stream order: runs of
  * `run` consecutive pairs per XCD (default 16, so consecutive pairs share

@@ -9,6 +9,18 @@
 
 #include "slamhip.h"
 
+// Timing-only ablation switches remove work from the ICP kernel and give
+// WRONG results (DESIGN.md section 3.1 cycle budget).  A product build refuses
+// them: only a build that also defines SLAM_TIMING_ONLY (tools/ab_build.sh
+// A/B libraries under ab/, never the in-tree libslamhip.so) may set them.
+#if !defined(SLAM_TIMING_ONLY) && (defined(SLAM_ABL_SUMS) || defined(SLAM_ABL_GROUP) || defined(SLAM_ABL_CERT) || \
+                                   defined(SLAM_ABL_STAGE2X) || defined(SLAM_NO_WINX) || defined(SLAM_KABSCH_ALL))
+#error "SLAM_ABL_* / SLAM_NO_WINX / SLAM_KABSCH_ALL are timing-only ablations: define SLAM_TIMING_ONLY as well (A/B builds only)"
+#endif
+#if defined(SLAM_TIMING_ONLY) && defined(SLAMHIP_PRODUCT_BUILD)
+#error "SLAM_TIMING_ONLY in a product build"
+#endif
+
 namespace slamhip {
 
 // Thread-local message of the last failing call (slam_last_error()).

@@ -823,6 +823,10 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
         bd.E = g.E0;
         bd.bz = g.bz;
     }
+    // the Schur path (pslot given) needs the direct block layout: without it the
+    // border solve below would run with no coupled rows and drop B entirely
+    if (nbd > 0 && pslot && !bd.D)
+        return fail(SLAM_EINVAL, "gn schur: no block layout (E=%d, %d slots, band %d scalars)", E, n_slots, nv_band);
     // the band (or the blocks) and the border rows are zeroed by the linearisation launch
     const int64_t B2 = static_cast<int64_t>(Wb) * Wb;
     double* z0 = bd.D ? bd.D : Hb;   // D and E0 are adjacent in the block workspace
@@ -917,6 +921,8 @@ static int gn_iteration(double* poses, int32_t N, const int32_t* ea, const int32
 
 extern "C" {
 
+int slam_gn_schur_supported(void) { return g_gn_solver != 1 && bcr_gj_default() ? 1 : 0; }
+
 int slam_gn_iteration_f64(double* poses, int32_t N, const int32_t* ea, const int32_t* eb, const double* tf,
                           const double* w, int32_t E, const int32_t* node_col, const int32_t* slot_rc,
                           const int32_t* slot_ptr, const int32_t* slot_items, int32_t n_slots, int32_t nv,
@@ -932,7 +938,7 @@ int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea, con
                                 double* work, double* out_chi2, int32_t* status, void* stream) {
     if (nv - nv_band < 1 || !pslot || n_pslot < 0 || (n_pslot > 0 && !pwork))
         return fail(SLAM_EINVAL, "gn schur: border %d, pslot %p, %d slots", nv - nv_band, pslot, n_pslot);
-    if (g_gn_solver == 1 || !bcr_gj_default())
+    if (!slam_gn_schur_supported())
         return fail(SLAM_EINVAL, "gn schur: needs the explicit-inverse cyclic reduction (solver mode %d)", g_gn_solver);
     return gn_iteration(poses, N, ea, eb, tf, w, E, node_col, slot_rc, slot_ptr, slot_items, n_slots, nv, W, nv_band,
                         nullptr, 0, work, out_chi2, status, stream, pslot, n_pslot, pwork);

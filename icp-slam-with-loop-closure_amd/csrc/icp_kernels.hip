@@ -2967,7 +2967,10 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                          wide_lds_bytes(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) <= kMaxLds;
     // angle pre-tier: the turning pairs on their own tier from the start (with
     // it, no phase-2 wide tier: measured slower, profiles/r05_shard_sweep8.txt)
-    const BulkGangInstance* apg = cfg_akind >= 2 ? pick_bulk_gang_instance(max_n1, cfg_akind) : nullptr;
+    // (bulk gangs run the pruned screen from an LDS-resident pc2: the same
+    // conditions as the phase-1 bulk gangs below)
+    const bool apg_ok = cfg_akind >= 2 && g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap;
+    const BulkGangInstance* apg = apg_ok ? pick_bulk_gang_instance(max_n1, cfg_akind) : nullptr;
     const int ap = (cfg_angle > 0 && (cfg_akind >= 2 ? apg != nullptr : wide_ok) && B <= kSortOneMax &&
                     g_sched_sort_one && B >= g_bulk_gang_below)
                        ? min(cfg_angle, B)
@@ -3148,6 +3151,11 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             if (ms != s && (hipEventRecord(side0->join3, ms) != hipSuccess || hipStreamWaitEvent(s, side0->join3, 0) != hipSuccess))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
             if (rc == 0) rc = launch(false, a, B, max_n1, max_n2, stream);
+            if (rc == 0 && ap) {   // the pre-tier's repair (its pairs are not in phase 2's order)
+                IcpArgs r = a;
+                r.order = order0;
+                rc = launch(false, r, ap, max_n1, max_n2, stream);
+            }
         }
     }
     if (ms != s && rc != 0) {   // an error after the pre-tier's fork: still join the phase stream before the free

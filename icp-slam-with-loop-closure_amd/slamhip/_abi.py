@@ -76,6 +76,7 @@ SIGNATURES = {
                                             c_ptr, c_ptr]),
     "slam_gn_set_fused_back": (c_int, [c_int]),
     "slam_gn_get_fused_back": (c_int, []),
+    "slam_gn_schur_supported": (c_int, []),
     "slam_gn_set_fused_wait": (c_int, [ctypes.c_uint32]),
 }
 

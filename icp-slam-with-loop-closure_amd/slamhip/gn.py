@@ -266,6 +266,11 @@ def schur_slots(nbr_rows, nv_band, W):
         return None, None
     if Wb <= 0 or not os.environ.get("SLAMHIP_GN_SCHUR", "1") == "1":
         return None, None
+    try:   # the solver this process runs must be the explicit-inverse reduction
+        if not int(_abi.lib().slam_gn_schur_supported()):
+            return None, None
+    except AttributeError:
+        return None, None
     nb = (nv_band + Wb - 1) // Wb
     nz = np.zeros(nb, dtype=bool)
     nz[np.asarray(nbr_rows, dtype=np.int64) // Wb] = True
@@ -287,6 +292,9 @@ def schur_slots(nbr_rows, nv_band, W):
 
 
 _PLANS = {}   # structure -> GnPlan (a pipeline re-optimises the same graph structure)
+# times the XCD-local back-substitution timed out and a run was repeated with
+# a launch per level (process-wide; bench.py reports it)
+FUSED_BACK_FALLBACKS = 0
 
 
 def plan_for(N, ea, eb, fixed=0):
@@ -393,19 +401,21 @@ class GaussNewton:
         lib = _abi.lib()
         # the fused back-substitution rests on the round-robin XCD dispatch; if a
         # wait times out (status bit 2) the steps are re-run without it
-        fused = self.plan.pslot is not None and self.plan.nv_band < self.plan.nv and lib.slam_gn_get_fused_back()
+        fused = bool(self.plan.pslot is not None and self.plan.nv_band < self.plan.nv and lib.slam_gn_get_fused_back())
         backup = self.poses.clone() if fused else None
         if graph is None:
             graph = self._eager_done and stream is None and iterations > 0
         if graph:
-            ent = self._graphs.get(iterations)
+            # keyed by the fused switch too: a graph captured with the fused
+            # kernel is never replayed after any instance's fallback turned it off
+            ent = self._graphs.get((iterations, fused))
             if ent is None:
                 chis = t.zeros(iterations, dtype=t.float64, device=self.poses.device)
                 g = t.cuda.CUDAGraph()
                 with t.cuda.graph(g):
                     for k in range(iterations):
                         self.iterate(chis[k:k + 1])
-                ent = self._graphs[iterations] = (g, chis)
+                ent = self._graphs[(iterations, fused)] = (g, chis)
             g, chis = ent
             g.replay()
         else:
@@ -419,6 +429,8 @@ class GaussNewton:
             import warnings
             warnings.warn("Gauss-Newton: the XCD-local back-substitution timed out (workgroup dispatch not "
                           "round-robin over the XCDs?); re-running with one launch per level", RuntimeWarning)
+            global FUSED_BACK_FALLBACKS
+            FUSED_BACK_FALLBACKS += 1
             lib.slam_gn_set_fused_back(0)
             self._graphs.clear()
             self.poses.copy_(backup)
@@ -440,8 +452,9 @@ def optimize(poses, ea, eb, tf, iterations=10, **kw):
     return s.host_poses(), chis
 
 
-def bench_c4(iterations=10, reps=3):
-    """GN iterations/s on config C4 (5k nodes / 20k edges), for bench.py."""
+def bench_c4(iterations=10, reps=5):
+    """GN iterations/s on config C4 (5k nodes / 20k edges), for bench.py: the
+    MEDIAN of `reps` timed runs of `iterations` steps (best and worst beside it)."""
     from . import synthetic
     t = dv.torch()
     guess, ea, eb, tf, _ = synthetic.lap_graph_c4()
@@ -450,14 +463,14 @@ def bench_c4(iterations=10, reps=3):
     plan_s = time.perf_counter() - t0
     s = GaussNewton(guess, ea, eb, tf, plan=plan)
     s.run(2)   # warm-up
-    best = None
+    dts = []
     for _ in range(reps):
         s.poses.copy_(dv.to_dev(guess, np.float64, s.poses.device))
         t.cuda.synchronize()
         t0 = time.perf_counter()
         chis = s.run(iterations)
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
+        dts.append(time.perf_counter() - t0)
+    med = float(np.median(dts))
     # end to end, as a caller sees it: host arrays in, plan (cold: symbolic
     # analysis; warm: cached structure), upload, `iterations` eager steps, poses out
     _PLANS.clear()
@@ -467,7 +480,11 @@ def bench_c4(iterations=10, reps=3):
         t0 = time.perf_counter()
         optimize(guess, ea, eb, tf, iterations)
         ends.append((time.perf_counter() - t0) * 1e3)
-    return {"gn_iters_per_sec": round(iterations / best, 2), "gn_ms_per_iter": round(best / iterations * 1e3, 4),
+    return {"gn_iters_per_sec": round(iterations / med, 2), "gn_ms_per_iter": round(med / iterations * 1e3, 4),
+            "gn_iters_per_sec_best_worst": [round(iterations / min(dts), 2), round(iterations / max(dts), 2)],
+            "gn_timing": "median of %d runs of %d iterations (HIP graph replay, host clock around each run)" % (
+                reps, iterations),
+            "gn_fused_back_fallbacks": FUSED_BACK_FALLBACKS,
             "gn_call_ms_cold_plan": round(ends[0], 2), "gn_call_ms_cached_plan": round(ends[1], 2),
             "gn_call_note": "optimize(): %d iterations from host arrays incl. plan, upload, eager launches, "
                             "download" % iterations,

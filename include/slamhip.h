@@ -226,6 +226,12 @@ int slam_gn_iteration_schur_f64(double* poses, int32_t N, const int32_t* ea,
  * one launch per level (0). */
 int slam_gn_set_fused_back(int on);
 int slam_gn_get_fused_back(void);
+/* 1 when slam_gn_iteration_schur_f64 can run in this process (the
+ * explicit-inverse cyclic reduction is the solver: not with
+ * slam_gn_set_solver(1) or the SLAMHIP_BCR_CHOL / SLAMHIP_BCR_LEGACY A/B
+ * switches), 0 otherwise: a bordered plan then takes
+ * slam_gn_iteration_bordered_f64. */
+int slam_gn_schur_supported(void);
 /* Diagnostics: the fused back-substitution's longest wait in s_memrealtime
  * ticks (0: the default 0.2 s); a tiny wait forces the timeout path. */
 int slam_gn_set_fused_wait(uint32_t ticks);

@@ -301,6 +301,11 @@ def test_gn_fused_back_substitution_and_fallback():
         chi_b = np.concatenate([b.run(1, graph=False), b.run(5, graph=True)])
         assert np.array_equal(chi_a, chi_b)
         assert np.array_equal(a.host_poses(), b.host_poses())
+        # another instance holding a graph captured WITH the fused kernel
+        d = gn.GaussNewton(guess, ea, eb, tf)
+        d.run(1, graph=False)
+        d.run(5, graph=True)
+        n_fb = gn.FUSED_BACK_FALLBACKS
         assert lib.slam_gn_set_fused_wait(1) == 0
         c = gn.GaussNewton(guess, ea, eb, tf)
         with warnings.catch_warnings(record=True) as w:
@@ -308,8 +313,15 @@ def test_gn_fused_back_substitution_and_fallback():
             chi_c = np.concatenate([c.run(1, graph=False), c.run(5, graph=False)])
         assert any("timed out" in str(x.message) for x in w)
         assert lib.slam_gn_get_fused_back() == 0
+        assert gn.FUSED_BACK_FALLBACKS == n_fb + 1
         assert np.array_equal(chi_a, chi_c)
         assert np.array_equal(a.host_poses(), c.host_poses())
+        # d must not replay its fused graph once the fallback turned the kernel off
+        import torch
+        d.poses.copy_(torch.as_tensor(guess, dtype=torch.float64).reshape(d.poses.shape))
+        chi_d = np.concatenate([d.run(1, graph=False), d.run(5, graph=True)])
+        assert np.array_equal(chi_a, chi_d)
+        assert np.array_equal(a.host_poses(), d.host_poses())
     finally:
         lib.slam_gn_set_fused_wait(0)
         lib.slam_gn_set_fused_back(1)
@@ -754,6 +766,9 @@ def test_schur_slots_match_a_numeric_reduction(nb, wb, nbd, seed):
     class FakeLib:
         def slam_gn_bcr_block_rows(self, nv, W):
             return wb
+
+        def slam_gn_schur_supported(self):
+            return 1
     with mock.patch.object(gn._abi, "lib", lambda: FakeLib()):
         pslot, blocks = gn.schur_slots(rows.astype(np.int32), n, wb)
     assert blocks.tolist() == coupled

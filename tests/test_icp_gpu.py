@@ -418,6 +418,45 @@ def test_default_schedule_large_batch(k):
     assert np.array_equal(phased.tf, single.tf) and np.array_equal(phased.err, single.err)
 
 
+def test_mid_batch_with_a_large_scan(k, oracle):
+    """A 2,100-pair batch (the automatic profile's 2,048-8,192 range: the angle
+    pre-tier as bulk gangs) in which ONE scan has 4,525 points, above the
+    LDS-resident candidate cap of 4,096: the pre-tier and the pruned screen
+    must step aside for the whole batch (the gangs stage pc2 in LDS), so
+    every pair, the turning ones included, equals the single launch bit for
+    bit and the oracle within 1e-9 — no EINVAL, no pair left unstarted."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 2100
+    seq, inits = _sequence_pairs(n, seed=21, n_beams=181)
+    rng = np.random.default_rng(11)
+    scans = list(seq.scans)
+    big = 1000
+    scans[big] = np.repeat(scans[big], 25, axis=0) + rng.normal(0.0, 1e-3, (25 * len(scans[big]), 2))
+    assert len(scans[big]) > 4096
+    ang = np.abs(np.arctan2(inits[:, 1, 0], inits[:, 0, 0]))
+    turning = np.flatnonzero(ang > 0.3)
+    assert len(turning) > 0
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    lib.slam_icp_gang_timeouts()   # clear
+    auto = k.icp_batch(scans, src, dst, inits, epsilon=0.05, max_iters=100)
+    assert lib.slam_icp_gang_timeouts() == 0
+    try:
+        assert lib.slam_icp_set_schedule(0, 1024) == 0
+        single = k.icp_batch(scans, src, dst, inits, epsilon=0.05, max_iters=100)
+    finally:
+        lib.slam_icp_set_schedule(-1, 1024)
+        lib.slam_icp_set_schedule_auto(1)
+    assert (auto.iters > 0).all()
+    assert np.array_equal(auto.iters, single.iters)
+    assert np.array_equal(auto.tf, single.tf) and np.array_equal(auto.err, single.err)
+    for b in sorted(set([big - 1, big]) | set(turning[:4].tolist())):
+        h, e = oracle.icp(homog(scans[b + 1]), homog(scans[b]), inits[b].copy(), 0.05, 100)
+        assert auto.iters[b] == len(h) - 1, b
+        assert np.abs(auto.tf[b] - h[-1]).max() <= TOL, b
+        assert abs(auto.err[b] - e) <= TOL * max(1.0, e), b
+
+
 def test_gangs_are_bit_identical(k):
     """Gangs (a pair's 64-query groups dealt over 2..17 workgroups that
     exchange their exact partial sums every iteration) and teams (parts = 0:

@@ -7,8 +7,10 @@
 Workload (BASELINE.json configs[2], "Batched ICP: 10k synthetic scan-pairs x
 1081 pts, 1->8 GPU sharding"): ONE synthetic scan stream of P+1 scans (P =
 10,000 by default; SURVEY.md §8(d) generator, seed 2025) whose P consecutive
-pairs (i, i-1) are sharded contiguously over the N ranks; each rank holds its
-shard resident in HBM and runs ``icp()`` on it with scripts/main.py's
+pairs (i, i-1) are sharded over the N ranks (``--shard``: contiguous slices,
+or cost-balanced by the turn of each pair's initial transform,
+slamhip.dist.balanced_shards); each rank holds its shard's scans resident in
+HBM and runs ``icp()`` on it with scripts/main.py's
 parameters (init = pose_to_mat(odom_i - odom_{i-1}), epsilon 0.05, max_iters
 100).  One step = one ``slam_icp_batch_f64`` launch over the rank's shard and,
 for N > 1, the RCCL all-gather of the resulting SE(2) edges (the exchange step
@@ -40,6 +42,7 @@ FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add per candidate distance
 # issue-bound candidate rate of the exact scan (~8 VALU
 # instructions per candidate): 256 CU x 2.4 GHz x 64 lanes / 8
 ISSUE_BOUND_EVALS_PER_S = 4.9e12
+DEFAULT_SHARD = "contiguous"
 KERNEL_SOURCES = ("icp-slam-with-loop-closure_amd/csrc/icp_kernels.hip", "icp-slam-with-loop-closure_amd/csrc/common.hpp")
 
 
@@ -85,6 +88,8 @@ def parse():
     p.add_argument("--sched-warm", type=int, default=-1,
                    help="1: phase 2 resumes with the saved search state (library default 0)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only for dry runs")
+    p.add_argument("--shard", default=DEFAULT_SHARD, choices=("contiguous", "balanced"),
+                   help="strong-scaling split of the pairs over the ranks (slamhip.dist)")
     return p.parse_args()
 
 
@@ -108,20 +113,24 @@ def init_dist(args):
 
 
 def make_workload(args, world, rank):
+    """This rank's pairs: (scans it holds, src, dst (local scan indices),
+    inits, every rank's pair-index list of the stream)."""
     from slamhip import se2, synthetic
     from slamhip import dist as sd
-    if not args.weak:
-        total = args.pairs
-        lo, hi, _ = sd.shard_range(total, world, rank)
-        seq = synthetic.make_sequence(total + 1, seed=2025, n_beams=args.beams)
-        scans = seq.scans[lo:hi + 1]
-        odo = seq.odometry[lo:hi + 1]
-    else:
-        seq = synthetic.make_sequence(args.pairs + 1, seed=2025 + rank, n_beams=args.beams)
-        scans, odo = seq.scans, seq.odometry
-    n = len(scans) - 1
+    seed = 2025 + (rank if args.weak else 0)
+    seq = synthetic.make_sequence(args.pairs + 1, seed=seed, n_beams=args.beams)
+    odo = seq.odometry
+    n = args.pairs
     inits = np.stack([se2.pose_to_mat(odo[i] - odo[i - 1]) for i in range(1, n + 1)]) if n else np.zeros((0, 3, 3))
-    return scans, inits
+    if args.weak or world == 1:
+        shards = [np.arange(n, dtype=np.int64)]
+        idx = shards[0]
+    else:
+        shards = (sd.balanced_shards(sd.turn_keys(inits), world) if args.shard == "balanced"
+                  else sd.contiguous_shards(n, world))
+        idx = shards[rank]
+    scans, src, dst = sd.local_scans(seq.scans, idx + 1, idx)
+    return scans, src, dst, inits[idx], shards
 
 
 def host_cpu():
@@ -161,7 +170,7 @@ def _oracle_pair(pc1, pc2, init, loop):
     return h[-1], float(e), len(h) - 1
 
 
-def cpu_baseline(scans, inits, sample, workers):
+def cpu_baseline(scans, src, dst, inits, sample, workers):
     """The reference's ICP restated in NumPy (oracle/icp_oracle.py, bit-exact
     with src/icp.py) on this host's cores, on bounded samples of this workload:
 
@@ -180,8 +189,8 @@ def cpu_baseline(scans, inits, sample, workers):
     n_all, n_aff, model = host_cpu()
 
     def job(i):
-        return (np.c_[scans[i + 1], np.ones(len(scans[i + 1]))], np.c_[scans[i], np.ones(len(scans[i]))],
-                inits[i].copy())
+        a, b = scans[src[i]], scans[dst[i]]
+        return np.c_[a, np.ones(len(a))], np.c_[b, np.ones(len(b))], inits[i].copy()
 
     def run(idx, loop, n_jobs):
         t0 = time.perf_counter()
@@ -359,7 +368,7 @@ def main():
     from slamhip import icp as k
 
     t_gen = time.perf_counter()
-    scans, inits = make_workload(args, world, rank)
+    scans, src, dst, inits, shards = make_workload(args, world, rank)
     B = len(inits)
     log(f"[rank {rank}] generated {B} pairs in {time.perf_counter() - t_gen:.1f}s")
     lib = _abi.lib()
@@ -382,12 +391,12 @@ def main():
         lib.slam_icp_set_schedule_warm(args.sched_warm)
     lib.slam_icp_set_screen(int(os.environ.get("SLAMHIP_SCREEN", "2")))
     ss = k.ScanSet(scans)
-    batch = k.IcpBatch(ss, np.arange(1, B + 1), np.arange(0, B), inits, epsilon=0.05, max_iters=100)
+    batch = k.IcpBatch(ss, src, dst, inits, epsilon=0.05, max_iters=100)
     from slamhip import dist as sd
     gathered = None
     if world > 1:
-        # SE(2) edge + error + iteration count of every pair, padded to the shard size
-        Bpad = max(sd.shard_range(args.pairs, world, 0)[2] if not args.weak else B, 1)
+        # SE(2) edge + error + iteration count of every pair, padded to the largest shard
+        Bpad = max(max(len(x) for x in shards) if not args.weak else B, 1)
         gathered = torch.empty((world, Bpad, sd.RESULT_WIDTH), dtype=torch.float64, device=ss.device)
         local_res = torch.zeros((Bpad, sd.RESULT_WIDTH), dtype=torch.float64, device=ss.device)
 
@@ -405,6 +414,9 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # exchange-tier timeouts (a gang / wide part whose partners were not all
+    # co-resident, repaired bit-identically but slow): counted over the timed steps
+    lib.slam_icp_gang_timeouts()   # read and clear
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -422,21 +434,29 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    timeouts = int(lib.slam_icp_gang_timeouts())
 
     res = batch.result()
-    n1 = ss.lens[1:B + 1]
-    n2 = ss.lens[0:B]
+    n1 = ss.lens[src]
+    n2 = ss.lens[dst]
     evals = float(np.sum(res.iters * n1 * n2))
     t = torch.tensor([dt, evals, float(B), float(res.iters.sum())], dtype=torch.float64,
                      device=ss.device if args.dist_backend == "nccl" else "cpu")
     per_rank = None
+    gather_ok = None
+    if world > 1 and not args.weak:
+        # the gathered SE(2) edges, put back in pair order, hold this rank's own results
+        tf_all, _, it_all = sd.unpack_shards(gathered, shards)
+        mine_idx = shards[rank]
+        gather_ok = bool(np.array_equal(tf_all[mine_idx], res.tf) and np.array_equal(it_all[mine_idx], res.iters))
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         t[0] = tmax[0]
         # every rank's shard and its kernel time (the slowest shard bounds the job)
-        mine = torch.tensor([kern_ms, float(B), dt / args.steps * 1e3], dtype=torch.float64, device=t.device)
+        mine = torch.tensor([kern_ms, float(B), dt / args.steps * 1e3, float(timeouts), float(res.iters.max())],
+                            dtype=torch.float64, device=t.device)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [[float(x) for x in r.cpu()] for r in allr]
@@ -508,11 +528,13 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8(d) ray-cast room, 1081 beams/270 deg, 0.01 m noise; EECS_3 unavailable offline)",
+        "exchange_timeouts": timeouts,
         "config": {"workload": "C3 batched ICP: consecutive scan pairs of a synthetic stream, "
                                "scripts/main.py params (eps 0.05, max_iters 100)",
                    "pairs_per_rank": B, "pairs_total": int(pairs_all), "points_per_scan": int(n1.max()),
                    "mean_icp_iterations": round(iters_all / pairs_all, 3),
-                   "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}"},
+                   "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}",
+                   "sharding": "weak (own stream per rank)" if args.weak else args.shard},
         "roofline": {
             # achieved = candidate evaluations per second against
             # the VALU issue bound 4.9e12 /s (= 24.5 TFLOP/s at 5 flops each)
@@ -554,20 +576,26 @@ def main():
                            "wall_ms_per_step": [round(r[2], 4) for r in per_rank],
                            "max_shard_pairs": int(max(r[1] for r in per_rank)),
                            "slowest_rank": int(np.argmax([r[0] for r in per_rank])),
+                           "exchange_timeouts": [int(r[3]) for r in per_rank],
+                           "all_gather_unpermuted_ok_rank0": gather_ok,
+                           "longest_pair_iterations": [int(r[4]) for r in per_rank],
+                           "shard": args.shard if not args.weak else "weak",
                            "note": "kernel_ms: HIP events around batch.launch() on each rank's stream; "
-                                   "wall: the rank's timed loop incl. the all-gather"}
+                                   "wall: the rank's timed loop incl. the all-gather; exchange_timeouts: "
+                                   "slam_icp_gang_timeouts() over the timed steps (repaired bit-identically)"}
     if world == 1 and not args.no_cpu_baseline:
         try:
             workers = args.cpu_workers or default_cpu_workers()
-            out["cpu_baseline"], ref = cpu_baseline(scans, inits, args.cpu_sample, workers)
+            out["cpu_baseline"], ref = cpu_baseline(scans, src, dst, inits, args.cpu_sample, workers)
             out["parity"] = parity_block(res, ref)
         except Exception as e:   # keep the GPU line even if the host pool fails
             out["cpu_baseline"] = {"error": repr(e)}
     if "parity" not in out:
         # no CPU baseline run (N > 1 or --no-cpu-baseline): a small vectorised sample
         idx = np.linspace(0, B - 1, min(B, 6)).astype(int) if B else []
-        ref = {int(i): _oracle_pair(np.c_[scans[i + 1], np.ones(len(scans[i + 1]))],
-                                    np.c_[scans[i], np.ones(len(scans[i]))], inits[i].copy(), False) for i in idx}
+        ref = {int(i): _oracle_pair(np.c_[scans[src[i]], np.ones(len(scans[src[i]]))],
+                                    np.c_[scans[dst[i]], np.ones(len(scans[dst[i]]))], inits[i].copy(), False)
+               for i in idx}
         if ref:
             out["parity"] = parity_block(res, ref)
             out["parity"]["scope"] = "rank 0's shard"

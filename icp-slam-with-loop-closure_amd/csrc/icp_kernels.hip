@@ -1926,8 +1926,11 @@ constexpr int kWideWaves = SLAM_WIDE_WAVES;
 constexpr int kWideBlock = 64 * kWideWaves;
 __host__ __device__ constexpr size_t wide_lds_bytes(int cap) {
     return red_doubles(kWideBlock) * sizeof(double) + static_cast<size_t>(cap) * (sizeof(double2) + sizeof(float2)) +
-           static_cast<size_t>(kWideWaves) * 3 * 64 * sizeof(uint32_t) + 8 * sizeof(double);
+           static_cast<size_t>(kWideWaves) * 3 * 64 * sizeof(uint32_t) + 8 * sizeof(double) + 64 * sizeof(int32_t);
 }
+// A wide slot's global slab (float4 units): the fp32 candidate pairs (cap / 2),
+// then one bounding box per chunk of kChunk candidates (cap / kChunk)
+__host__ __device__ constexpr int64_t wide_slab_f4(int cap) { return cap / 2 + cap / kChunk; }
 
 // src/icp.py:22-46 + 64-67 from the 16 exact partial sums (lane q holds value
 // q, every lane the same T): the Kabsch update of icp_kernel, one wave.
@@ -1984,7 +1987,7 @@ __global__ __launch_bounds__(256) void wide_prep_kernel(IcpArgs a, float2* __res
     const int s2 = a.dst_scan[b];
     const int64_t o2 = a.scan_off[s2];
     const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
-    float2* dst = wcand + static_cast<int64_t>(slot) * a.cand_cap;
+    float2* dst = wcand + 2 * static_cast<int64_t>(slot) * wide_slab_f4(a.cand_cap);
     for (int j = threadIdx.x; j < a.cand_cap; j += 256) {
         float x = kSentinel, y = kSentinel;
         if (j < n2) {
@@ -1993,6 +1996,22 @@ __global__ __launch_bounds__(256) void wide_prep_kernel(IcpArgs a, float2* __res
             y = static_cast<float>(p.y);
         }
         cf_put(dst, j, x, y);
+    }
+    // per chunk: the box of its real candidates' fp32 points (a chunk of
+    // sentinels only gets a box at the sentinel: its bound is +inf)
+    float4* box = reinterpret_cast<float4*>(dst) + a.cand_cap / 2;
+    for (int c = threadIdx.x; c < a.cand_cap / kChunk; c += 256) {
+        float4 bx = make_float4(kSentinel, kSentinel, kSentinel, kSentinel);
+        for (int j = c * kChunk; j < min((c + 1) * kChunk, n2); ++j) {
+            const double2 p = a.pts[o2 + j];
+            const float x = static_cast<float>(p.x), y = static_cast<float>(p.y);
+            const bool first = j == c * kChunk;
+            bx.x = first ? x : fminf(bx.x, x);
+            bx.y = first ? y : fminf(bx.y, y);
+            bx.z = first ? x : fmaxf(bx.z, x);
+            bx.w = first ? y : fmaxf(bx.w, y);
+        }
+        box[c] = bx;
     }
 }
 
@@ -2007,6 +2026,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
     float2* candf = reinterpret_cast<float2*>(cand + cap);
     uint32_t* xs = reinterpret_cast<uint32_t*>(candf + cap);    // [NW][3][64]: M1, chunk, M2 per wave
     double* tb = reinterpret_cast<double*>(xs + NW * 3 * 64);   // the next T (6) and the flag
+    int32_t* pm = reinterpret_cast<int32_t*>(tb + 8);           // [64]: the group's last matches (wave 0 -> all)
 
     const int parts = a.gang;
     const int bx = static_cast<int>(blockIdx.x);
@@ -2051,7 +2071,18 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
     const int i = part * 64 + lane;
     const bool valid = i < n1;
     const int nch = (n2 + kChunk - 1) / kChunk;
-    const int c_lo = wave * nch / NW, c_hi = (wave + 1) * nch / NW;   // this wave's chunks
+    // the slot's fp32 candidate pairs and chunk boxes (wide_prep_kernel), read
+    // through scalar loads; wave w scans the chunks w, w + NW, ... (interleaved:
+    // the few chunks a group's queries need spread over the waves)
+    const float4* __restrict__ cg = wcand + static_cast<int64_t>(slot) * wide_slab_f4(cap);
+    const float4* __restrict__ cbox = cg + cap / 2;
+    // pruning (round 6): from the second iteration of a launch on, a lane's last
+    // match j0 and its neighbour bound the runner-up: U = max(d32(j0), d32(j0 +- 1))
+    // >= M2 >= M1, so a chunk whose box lies farther than U from the lane's
+    // query holds neither the minimum nor the runner-up; it is skipped when no
+    // lane of the wave needs it.  The certification takes min(M2, U) as its
+    // bound on the other candidates (skipped ones are > U): results unchanged.
+    bool warm = false;
     uint64_t* slots = a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32;
     // diagnostics (a.stamps != NULL): s_memtime per phase of wave 0 of every
     // part, stamps[256 + 16 * part + phase] (tools/wide_stamps.py)
@@ -2079,9 +2110,21 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
         //      their bits order as unsigned integers) ---------------------------
         uint32_t M1 = 0xffffffffu, M2 = 0xffffffffu;
         int C1 = 0;
+        uint32_t U = 0x7f800000u;   // +inf: no pruning
         if (ps.screen) {
-            const float4* __restrict__ cg = wcand + static_cast<int64_t>(slot) * (cap / 2);   // uniform: s_load
-            for (int c = c_lo; c < c_hi; ++c) {
+            if (warm) {
+                const int j0 = pm[lane];
+                const int j1 = j0 + 1 < n2 ? j0 + 1 : j0 - 1;   // warm implies n2 >= 2
+                const float2 a0 = cf_at(candf, j0), a1 = cf_at(candf, j1);
+                U = valid ? max(__float_as_uint(screen_d32(a0.x, a0.y, fx, fy)),
+                                __float_as_uint(screen_d32(a1.x, a1.y, fx, fy)))
+                          : 0u;
+            }
+            for (int c = wave; c < nch; c += NW) {
+                if (warm) {
+                    const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, cbox[c]);
+                    if (!__builtin_amdgcn_ballot_w64(valid && __float_as_uint(lb) <= U)) continue;   // uniform
+                }
                 const float4* cp = cg + c * (kChunk / 2);
                 uint32_t cm = 0xffffffffu;
 #pragma unroll
@@ -2099,18 +2142,19 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
         tstamp(0);
         xs[(wave * 3 + 0) * 64 + lane] = M1;
         xs[(wave * 3 + 1) * 64 + lane] = static_cast<uint32_t>(C1);
-        xs[(wave * 3 + 2) * 64 + lane] = M2;
+        xs[(wave * 3 + 2) * 64 + lane] = min(M2, U);   // (every wave holds the same U)
         __syncthreads();
         tstamp(1);
         if (wave == 0) {
-            // merge in candidate (wave) order: strict < keeps the first chunk on ties
+            // merge: the smallest chunk minimum, the lowest chunk on ties (the
+            // waves' chunks interleave), and the second smallest over all chunks
             uint32_t m1 = 0xffffffffu, m2 = 0xffffffffu;
             int c1 = 0;
 #pragma unroll
             for (int w = 0; w < NW; ++w) {
                 const uint32_t a1 = xs[(w * 3 + 0) * 64 + lane], a2 = xs[(w * 3 + 2) * 64 + lane];
                 const int ac = static_cast<int>(xs[(w * 3 + 1) * 64 + lane]);
-                c1 = a1 < m1 ? ac : c1;
+                c1 = (a1 < m1 || (a1 == m1 && ac < c1)) ? ac : c1;
                 m2 = min(max(m1, a1), min(m2, a2));
                 m1 = min(m1, a1);
             }
@@ -2183,6 +2227,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
                 }
             }
             tstamp(3);
+            pm[lane] = bi;   // the next iteration's prediction (read after the barrier below)
             // sums (as icp_kernel step 4), this group's 64 queries
             const double2 c = *reinterpret_cast<const double2*>(pconst + kPcX);
             const double2 gmv = *reinterpret_cast<const double2*>(pconst + kGm1);
@@ -2257,6 +2302,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
         }
         T.m00 = uniform_d(tb[0]); T.m01 = uniform_d(tb[1]); T.m02 = uniform_d(tb[2]);
         T.m10 = uniform_d(tb[3]); T.m11 = uniform_d(tb[4]); T.m12 = uniform_d(tb[5]);
+        warm = n2 >= 2;
     }
 }
 
@@ -2562,6 +2608,10 @@ static thread_local float g_angle_thresh = 0.3f;
 // 2 / 3: bulk gangs of that many ordinary workgroups (cheap enough for the
 // larger shards' dozens of turning pairs)
 static thread_local int g_angle_kind = 0;
+// with a gang pre-tier (kind 2 / 3): its first g_angle_mix turning pairs (the
+// largest turns) on wide workgroups instead, g_angle_mix_share per CU (0: none)
+static thread_local int g_angle_mix = 0;
+static thread_local int g_angle_mix_share = 2;
 // Automatic tier profile by batch size (the default; any explicit tier setter
 // turns it off, slam_icp_set_schedule_auto(1) turns it back on), measured on
 // every rank's shard of the 10k C3 stream (tools/shard_sweep.py,
@@ -2834,7 +2884,7 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
                                                                     const int32_t* __restrict__ ids,
                                                                     int32_t* __restrict__ k_dev,
                                                                     const double* __restrict__ init, int32_t kmax,
-                                                                    int32_t* __restrict__ out_iters) {
+                                                                    int32_t* __restrict__ out_iters, int32_t kmix = -1) {
     constexpr int WAVES = kSortBlock / 64;
     constexpr int PER = kSortOneMax / kSortBlock;
     __shared__ int base[kNB];
@@ -2880,6 +2930,7 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
         }
         if constexpr (MODE == 1) {
             if (lane == 0) *k_dev = min(base[kSchedBuckets], kmax);   // turning pairs precede bucket 256
+            if (lane == 0 && kmix >= 0) k_dev[1] = min(base[kSchedBuckets], kmix);   // the mixed pre-tier's wide part
         }
     }
     __syncthreads();
@@ -2931,12 +2982,15 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     // the tier profile: explicit settings, or the automatic one by batch size
     int cfg_heads = g_sched_heads, cfg_gangs = g_sched_gangs, cfg_parts = g_sched_gang_parts;
     int cfg_wide = g_sched_wide, cfg_share = g_wide_share, cfg_angle = g_angle_max, cfg_akind = g_angle_kind;
+    int cfg_mix = g_angle_mix, cfg_mix_share = g_angle_mix_share;
     int tiers_below = g_tiers_below;
     if (g_sched_auto) {
         cfg_wide = 0;
         cfg_share = 1;
         cfg_parts = 4;
         cfg_akind = 0;
+        cfg_mix = 0;
+        cfg_mix_share = 2;
         if (B < kAutoSmall) {
             cfg_heads = 0;
             cfg_gangs = 0;
@@ -2975,13 +3029,15 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                     g_sched_sort_one && B >= g_bulk_gang_below)
                        ? min(cfg_angle, B)
                        : 0;
+    // mixed pre-tier: its first `mix` pairs on wide workgroups, the rest on the gangs
+    const int mix = (ap > 0 && apg && wide_ok && cfg_mix > 0) ? min(cfg_mix, ap) : 0;
     const int Wd = wide_ok && ap == 0 ? min(cfg_wide, heads) : 0;
     const int G = gang_ok ? max(0, min(cfg_gangs, heads - Wd)) : 0;
     const size_t wide_slot_words = static_cast<size_t>(Wd) * 2 * wide_parts * 32;
     const size_t gang_slot_bytes =
         (static_cast<size_t>(G) * 2 * max(parts, 1) * 32 + wide_slot_words) * sizeof(uint64_t);
-    const size_t wide_cand_bytes = static_cast<size_t>(Wd) * ((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk *
-                                   sizeof(float2);
+    const size_t wide_cand_bytes =
+        static_cast<size_t>(Wd) * wide_slab_f4(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk) * sizeof(float4);
     // bulk gangs for a batch too small to fill the GPU with whole pairs
     const BulkGangInstance* bg =
         B < g_bulk_gang_below && g_bulk_gang_parts >= 2 && g_forced_instance < 0 && g_screen == 2 && max_n2 <= kCandCap
@@ -2997,9 +3053,11 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                                            : 0;
     // angle pre-tier: order0 (B), its count (device), exchange slots, fp32 candidates
     const size_t cand_cap_w = static_cast<size_t>(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk);
-    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * max(wide_parts, 3) * 32;
-    const size_t ap_bytes = ap ? ((nb + 1) * sizeof(int32_t) + 255) / 256 * 256 + ap_slot_words * sizeof(uint64_t) +
-                                     static_cast<size_t>(ap) * cand_cap_w * sizeof(float2)
+    // (a mixed pre-tier: the wide part's slots first, then the gangs' by slot index)
+    const size_t ap_mix_words = static_cast<size_t>(mix) * 2 * wide_parts * 32;
+    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * max(wide_parts, 3) * 32 + ap_mix_words;
+    const size_t ap_bytes = ap ? ((nb + 2) * sizeof(int32_t) + 255) / 256 * 256 + ap_slot_words * sizeof(uint64_t) +
+                                     static_cast<size_t>(ap) * wide_slab_f4(static_cast<int>(cand_cap_w)) * sizeof(float4)
                                : 0;
     const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes + ap_bytes;
     void* ws = nullptr;
@@ -3013,9 +3071,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     uint64_t* bulk_slots =
         reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + sched_bytes + gang_slot_bytes + wide_cand_bytes);
     char* ap0 = static_cast<char*>(ws) + sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes;
-    int32_t* order0 = ap ? reinterpret_cast<int32_t*>(ap0) : nullptr;   // [B] + the count at order0[B]
+    int32_t* order0 = ap ? reinterpret_cast<int32_t*>(ap0) : nullptr;   // [B] + the counts at order0[B], [B + 1]
     int32_t* ap_k = ap ? order0 + nb : nullptr;
-    uint64_t* ap_slots = ap ? reinterpret_cast<uint64_t*>(ap0 + ((nb + 1) * sizeof(int32_t) + 255) / 256 * 256) : nullptr;
+    uint64_t* ap_slots = ap ? reinterpret_cast<uint64_t*>(ap0 + ((nb + 2) * sizeof(int32_t) + 255) / 256 * 256) : nullptr;
     float2* ap_cand = ap ? reinterpret_cast<float2*>(ap_slots + ap_slot_words) : nullptr;
     IcpArgs a = args;
     a.phase_cap = probe;
@@ -3043,7 +3101,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         hipLaunchKernelGGL(sched_sort_one_kernel<1>, dim3(1), dim3(kSortBlock), 0, s, args.out_iters,
                            static_cast<const float*>(nullptr), B, g_angle_thresh, order0, ap_slots,
                            static_cast<int64_t>(ap_slot_words), static_cast<const int32_t*>(nullptr), ap_k, args.init, ap,
-                           args.out_iters);
+                           args.out_iters, mix > 0 ? mix : -1);
         if (hipEventRecord(side0->fork, s) != hipSuccess || hipStreamWaitEvent(side0->stream3, side0->fork, 0) != hipSuccess)
             rc = fail(SLAM_EHIP, "icp scheduler: fork");
         else
@@ -3051,8 +3109,14 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         IcpArgs w = args;
         w.order = order0;
         w.take_lt = ap_k;
+        if (rc == 0 && mix > 0) {   // the largest turns on wide workgroups (slots below ap_k[1])
+            IcpArgs wm = w;
+            wm.take_lt = ap_k + 1;
+            rc = launch_wide(wm, mix, max_n1, max_n2, s, ap_slots, ap_cand, cfg_mix_share);
+            w.skip_lt = ap_k + 1;   // the gangs take the slots from there to ap_k[0]
+        }
         if (rc == 0)
-            rc = apg ? launch_bulk_gangs(w, ap, apg, max_n2, s, ap_slots)
+            rc = apg ? launch_bulk_gangs(w, ap, apg, max_n2, s, ap_slots + ap_mix_words)
                      : launch_wide(w, ap, max_n1, max_n2, s, ap_slots, ap_cand, cfg_share);
         a.order = order0;
         a.skip_lt = ap_k;
@@ -3288,6 +3352,13 @@ int slam_icp_set_angle_tier_kind(int kind) {
     g_sched_auto = 0;
     return ok();
 }
+int slam_icp_set_angle_tier_mix(int wide_pairs, int share) {
+    if (wide_pairs < 0 || share < 1 || share > 8) return fail(SLAM_EINVAL, "angle tier mix %d, share %d", wide_pairs, share);
+    g_angle_mix = wide_pairs;
+    g_angle_mix_share = share;
+    g_sched_auto = 0;
+    return ok();
+}
 // The automatic tier profile by batch size (1, default) or the explicit
 // settings (0; any tier setter selects them).  1 also restores the explicit
 // settings' defaults (64 heads, 24 gangs of 4, no wide tier, no angle tier).
@@ -3302,6 +3373,8 @@ int slam_icp_set_schedule_auto(int on) {
         g_angle_max = 0;
         g_angle_thresh = 0.3f;
         g_angle_kind = 0;
+        g_angle_mix = 0;
+        g_angle_mix_share = 2;
     }
     return ok();
 }

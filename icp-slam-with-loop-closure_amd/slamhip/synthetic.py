@@ -124,8 +124,14 @@ class Sequence:
     scans: list             # S x (m_i, 2)
 
 
-def make_sequence(n_scans: int, seed: int, n_beams=N_BEAMS) -> Sequence:
-    """A scan stream like the reference's LCM logs (src/dataloader.py:106-125)."""
+def make_sequence(n_scans: int, seed: int, n_beams=N_BEAMS, dropout=0.0) -> Sequence:
+    """A scan stream like the reference's LCM logs (src/dataloader.py:106-125).
+
+    dropout > 0: ragged scans — every scan loses a fraction U(0, dropout) of
+    its beams at random positions, as returns with range <= 0.05 m that
+    src/dataloader.py:47-55 filters out (dropout 0.35: 700-1081 points of
+    1081).  Drawn from a separate generator: the stream itself (world, path,
+    odometry, noise) is the same as without dropout."""
     rng = np.random.default_rng(seed)
     world = make_world(rng)
     truth = random_walk(world, rng, n_scans)
@@ -133,6 +139,12 @@ def make_sequence(n_scans: int, seed: int, n_beams=N_BEAMS) -> Sequence:
     odom[:, 0:2] += rng.normal(0.0, 0.01, size=(n_scans, 2))
     odom[:, 2] += rng.normal(0.0, 0.005, size=n_scans)
     scans = scans_from_poses(world, truth, rng, n_beams=n_beams)
+    if dropout > 0.0:
+        drng = np.random.default_rng([seed, 0x5ca7])
+        for i, sc in enumerate(scans):
+            keep = drng.random(len(sc)) >= drng.uniform(0.0, dropout)
+            keep[drng.integers(len(sc))] = True   # never empty
+            scans[i] = sc[keep]
     return Sequence(world, truth, odom, scans)
 
 

@@ -335,6 +335,10 @@ int slam_icp_set_angle_tier(int max_pairs, float thresh_rad);
 /* Diagnostics: the angle pre-tier's kind, 0 the wide tier, 2 / 3 bulk gangs
  * of that many ordinary workgroups per pair. */
 int slam_icp_set_angle_tier_kind(int kind);
+/* Diagnostics: with a gang pre-tier (kind 2 / 3), its first wide_pairs
+ * turning pairs (the largest turns) run on wide workgroups, `share` per CU,
+ * the rest on the gangs (0: none).  Bit-identical. */
+int slam_icp_set_angle_tier_mix(int wide_pairs, int share);
 /* The scheduler's automatic tier profile by batch size (1, default; DESIGN.md
  * section 6): below 2,048 pairs 24 pre-tier pairs on wide workgroups; 2,048 -
  * 8,192 pairs 96 pre-tier pairs on gangs of 3 plus 64 phase-2 heads, the first

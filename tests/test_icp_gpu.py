@@ -497,6 +497,15 @@ def test_gangs_are_bit_identical(k):
             runs[("angle", amax, athr, gangs, kind)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05,
                                                                    max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() == 0
+        # the mixed pre-tier: its largest turns on wide workgroups, the rest on gangs of 3
+        for amax, mix, share in ((48, 8, 2), (96, 16, 4), (24, 24, 1)):
+            assert lib.slam_icp_set_angle_tier(amax, 0.05) == 0
+            assert lib.slam_icp_set_angle_tier_kind(3) == 0
+            assert lib.slam_icp_set_angle_tier_mix(mix, share) == 0
+            runs[("mix", amax, mix, share)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100,
+                                                          history=True)
+            assert lib.slam_icp_gang_timeouts() == 0
+        assert lib.slam_icp_set_angle_tier_mix(0, 2) == 0
         assert lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE) == 0
         assert lib.slam_icp_set_angle_tier_kind(0) == 0
         # bulk gangs: both phases' bulk as gangs of 2 / 3 ordinary workgroups

@@ -1,13 +1,19 @@
 """Strong-scaling projection on ONE GPU, done the way bench.py shards: every
-rank's shard of the ONE 10k C3 stream (slamhip.dist.shard_range over N ranks,
-N = 2, 4, 8) timed on its own (HIP events, median of 5 launches), under each
-scheduler setting "heads,gangs,parts,wide,share[,probe[,sort_one[,tier_limit[,xcd_map[,angle_max[,angle_centirad[,angle_kind]]]]]]]".  The
-projected N-GPU time is the slowest shard (bench.py takes the max over ranks).
+rank's shard of ONE C3 stream over N ranks (N = 2, 4, 8) timed on its own
+(HIP events, median of 5 launches), under each scheduler setting
+"heads,gangs,parts,wide,share[,probe[,sort_one[,tier_limit[,xcd_map[,angle_max[,angle_centirad[,angle_kind[,mix,mix_share]]]]]]]]"
+or "auto" (the library's automatic tier profile).  The projected N-GPU time
+is the slowest shard (bench.py takes the max over ranks).
 (bench.py --pairs P builds ANOTHER stream of P pairs: synthetic.make_sequence
 draws its noise after the whole trajectory, so a shorter stream is not a
 prefix of the 10k one.)  GPU only.
 
     python tools/shard_sweep.py [setting ... | auto]
+
+Environment: SHARD_TOTAL (10000 pairs), SHARD_N (2,4,8), SHARD_SEED (2025:
+the C3 stream), SHARD_DROPOUT (0: 1081-point scans; 0.35: ragged 700-1081),
+SHARD_MODE (contiguous | balanced | both: slamhip.dist.contiguous_shards /
+balanced_shards).
 """
 import os
 import sys
@@ -25,19 +31,27 @@ def main():
     from slamhip import dist as sd
     from slamhip import icp as k
     lib = _abi.lib()
-    settings = sys.argv[1:] or ["64,24,4,0,1"]
+    settings = sys.argv[1:] or ["auto"]
     total = int(os.environ.get("SHARD_TOTAL", "10000"))
-    seq = synthetic.make_sequence(total + 1, seed=2025)
+    seed = int(os.environ.get("SHARD_SEED", "2025"))
+    dropout = float(os.environ.get("SHARD_DROPOUT", "0"))
+    modes = {"both": ["contiguous", "balanced"]}.get(os.environ.get("SHARD_MODE", "both"),
+                                                     [os.environ.get("SHARD_MODE", "both")])
+    seq = synthetic.make_sequence(total + 1, seed=seed, dropout=dropout)
+    lens = np.array([len(s) for s in seq.scans])
+    print(f"stream seed {seed} dropout {dropout}: {total} pairs, scans of {lens.min()}-{lens.max()} points", flush=True)
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, total + 1)])
+    keys = sd.turn_keys(inits)
     ss = k.ScanSet(seq.scans)
     ranks = [int(x) for x in os.environ.get("SHARD_N", "2,4,8").split(",")]
     batches = {}
-    for n in [1] + ranks:
-        for r in range(n):
-            lo, hi, _ = sd.shard_range(total, n, r)
-            batches[(n, r)] = k.IcpBatch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi],
-                                         epsilon=0.05, max_iters=100)
+    for mode in modes:
+        for n in [1] + ranks:
+            shards = sd.balanced_shards(keys, n) if mode == "balanced" else sd.contiguous_shards(total, n)
+            for r, idx in enumerate(shards):
+                batches[(mode, n, r)] = (idx, k.IcpBatch(ss, idx + 1, idx, inits[idx], epsilon=0.05, max_iters=100))
     ref = {}
+    full = {}
 
     def timed(b, reps=5):
         b.launch()
@@ -70,24 +84,34 @@ def main():
             if st != "auto":
                 assert lib.slam_icp_set_angle_tier(v[9] if len(v) > 9 else 0, (v[10] if len(v) > 10 else 30) / 100.0) == 0
                 assert lib.slam_icp_set_angle_tier_kind(v[11] if len(v) > 11 else 0) == 0
-            line = []
-            t1 = None
-            for n in [1] + ranks:
-                ts = []
-                for r in range(n):
-                    b = batches[(n, r)]
-                    ts.append(timed(b, 3 if n == 1 else 5))
-                    res = b.result()
-                    key = (n, r)
-                    if key not in ref:
-                        ref[key] = res
-                    elif not (np.array_equal(res.tf, ref[key].tf) and np.array_equal(res.iters, ref[key].iters)):
-                        line.append(f"MISMATCH n{n}r{r}")
-                mx = max(ts)
-                if n == 1:
-                    t1 = mx
-                line.append(f"N{n}: max {mx:.3f} ({t1 / mx:.2f}x) shards " + " ".join(f"{t:.3f}" for t in ts))
-            print(f"h,g,k,w,s {st:16s} | " + " | ".join(line), flush=True)
+                assert lib.slam_icp_set_angle_tier_mix(v[12] if len(v) > 12 else 0, v[13] if len(v) > 13 else 2) == 0
+            for mode in modes:
+                line = []
+                t1 = None
+                lib.slam_icp_gang_timeouts()   # clear
+                for n in [1] + ranks:
+                    ts = []
+                    for r in range(n):
+                        idx, b = batches[(mode, n, r)]
+                        ts.append(timed(b, 3 if n == 1 else 5))
+                        res = b.result()
+                        if n == 1:
+                            full.setdefault("tf", res.tf)
+                            full.setdefault("iters", res.iters)
+                        # every shard bit-identical to the full batch's rows
+                        if not (np.array_equal(res.tf, full["tf"][idx]) and np.array_equal(res.iters, full["iters"][idx])):
+                            line.append(f"MISMATCH n{n}r{r}")
+                        key = (mode, n, r)
+                        if key not in ref:
+                            ref[key] = res
+                    mx = max(ts)
+                    if n == 1:
+                        t1 = mx
+                    its = [int(full["iters"][batches[(mode, n, r)][0]].max()) for r in range(n)]
+                    line.append(f"N{n}: max {mx:.3f} ({t1 / mx:.2f}x) shards " + " ".join(f"{t:.3f}" for t in ts) +
+                                (f" longest {its}" if n > 1 else ""))
+                tmo = lib.slam_icp_gang_timeouts()
+                print(f"{mode:10s} {st:16s} | " + " | ".join(line) + f" | timeouts {tmo}", flush=True)
     finally:
         lib.slam_icp_set_schedule_auto(1)
         lib.slam_icp_set_schedule(-1, 1024)
@@ -95,6 +119,7 @@ def main():
         lib.slam_icp_set_tier_limit(0)
         lib.slam_icp_set_xcd_map(-1)
         lib.slam_icp_set_angle_tier(0, 0.3)
+        lib.slam_icp_set_schedule_auto(1)
 
 
 if __name__ == "__main__":

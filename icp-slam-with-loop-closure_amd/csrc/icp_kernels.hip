@@ -1924,9 +1924,11 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
 #endif
 constexpr int kWideWaves = SLAM_WIDE_WAVES;
 constexpr int kWideBlock = 64 * kWideWaves;
-__host__ __device__ constexpr size_t wide_lds_bytes(int cap) {
-    return red_doubles(kWideBlock) * sizeof(double) + static_cast<size_t>(cap) * (sizeof(double2) + sizeof(float2)) +
-           static_cast<size_t>(kWideWaves) * 3 * 64 * sizeof(uint32_t) + 8 * sizeof(double) + 64 * sizeof(int32_t);
+__host__ __device__ constexpr size_t wide_lds_bytes(int cap, int groups = 1) {
+    return red_doubles(kWideBlock * groups) * sizeof(double) +
+           static_cast<size_t>(cap) * (sizeof(double2) + sizeof(float2)) +
+           static_cast<size_t>(kWideWaves * groups) * 3 * 64 * sizeof(uint32_t) + 24 * sizeof(double) +
+           static_cast<size_t>(groups) * 64 * sizeof(int32_t);
 }
 // A wide slot's global slab (float4 units): the fp32 candidate pairs (cap / 2),
 // then one bounding box per chunk of kChunk candidates (cap / kChunk)
@@ -2015,28 +2017,38 @@ __global__ __launch_bounds__(256) void wide_prep_kernel(IcpArgs a, float2* __res
     }
 }
 
-__global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const float4* __restrict__ wcand) {
+// G query groups per workgroup (1: 8 waves; 2: 16 waves, the workgroup a CU
+// of its own, round 6): group gq = wave % G (its leader, wave gq, on SIMD gq),
+// its NW waves wave = gq + G w.  With G = 2 the two leaders add their exact
+// partial sums (order-free) before the one exchange of the workgroup, so a
+// 1081-point pair runs on 9 workgroups instead of 17.
+template <int G>
+__global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a, const float4* __restrict__ wcand) {
     constexpr int NW = kWideWaves;
+    constexpr int WAVES = NW * G;
+    constexpr int WBLK = 64 * WAVES;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* red0 = reinterpret_cast<double*>(smem);
-    double* red1 = red0 + NW * 16;
-    double* pconst = red0 + 2 * NW * 16;
-    double2* cand = reinterpret_cast<double2*>(smem + red_doubles(kWideBlock) * sizeof(double));
+    double* red1 = red0 + WAVES * 16;
+    double* pconst = red0 + 2 * WAVES * 16;
+    double2* cand = reinterpret_cast<double2*>(smem + red_doubles(WBLK) * sizeof(double));
     const int cap = a.cand_cap;
     float2* candf = reinterpret_cast<float2*>(cand + cap);
-    uint32_t* xs = reinterpret_cast<uint32_t*>(candf + cap);    // [NW][3][64]: M1, chunk, M2 per wave
-    double* tb = reinterpret_cast<double*>(xs + NW * 3 * 64);   // the next T (6) and the flag
-    int32_t* pm = reinterpret_cast<int32_t*>(tb + 8);           // [64]: the group's last matches (wave 0 -> all)
+    uint32_t* xs = reinterpret_cast<uint32_t*>(candf + cap);       // [WAVES][3][64]: M1, chunk, M2 per wave
+    double* tb = reinterpret_cast<double*>(xs + WAVES * 3 * 64);   // the next T (6) and the flag
+    double* gsum = tb + 8;                                         // [16]: group 1's partial sums (G = 2)
+    int32_t* pm = reinterpret_cast<int32_t*>(gsum + 16);           // [G][64]: the groups' last matches
 
     const int parts = a.gang;
     const int bx = static_cast<int>(blockIdx.x);
     const int slot = (bx / (8 * parts)) * 8 + (bx & 7);   // a pair's workgroups on one XCD
-    const int part = (bx >> 3) % parts;                     // = its 64-query group
+    const int part = (bx >> 3) % parts;                     // = its G 64-query groups
     if (slot >= a.n_gangs || (a.take_lt && slot >= *a.take_lt)) return;
     const int b = a.order ? a.order[slot] : slot;
     if (b < 0) return;   // padding (uniform)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gq = wave % G, wg = wave / G;   // query group in the workgroup, wave in the group
     int it0 = 0;
     if (a.resume) {
         const int s = a.out_iters[b];
@@ -2049,7 +2061,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
     const int n2 = static_cast<int>(a.scan_off[s2 + 1] - o2);
     const double2* __restrict__ p1 = a.pts + o1;
     const double2* __restrict__ p2 = a.pts + o2;
-    if (n1 < 1 || n2 < 1 || n1 > 64 * parts || n2 > cap) {
+    if (n1 < 1 || n2 < 1 || n1 > 64 * G * parts || n2 > cap) {
         if (tid == 0 && part == 0) {
             a.out_iters[b] = kBadBounds;
             a.out_err[b] = __builtin_nan("");
@@ -2058,8 +2070,8 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
         return;
     }
     if (tid == 0 && part == 0) trace_mark(a, b, 0);
-    const PairSetup ps = stage_pair<kWideBlock, true, false>(a, n1, n2, p1, p2, true, cand, candf, nullptr, red0,
-                                                             red1, pconst);
+    const PairSetup ps = stage_pair<WBLK, true, false>(a, n1, n2, p1, p2, true, cand, candf, nullptr, red0, red1,
+                                                       pconst);
     SE2 T = load_se2((it0 > 0 ? a.out_tf : a.init) + 9 * static_cast<int64_t>(b));
     if (a.rotation_only) {
         T.m02 = 0.0;
@@ -2068,7 +2080,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
     double* hist = a.hist_stride > 0 ? a.out_hist + static_cast<int64_t>(b) * a.hist_stride * 9 : nullptr;
     if (hist && tid == 0 && part == 0 && it0 == 0) store_se2(hist, T);
     double last_err = it0 > 0 ? a.out_err[b] : 0.0;
-    const int i = part * 64 + lane;
+    const int i = (part * G + gq) * 64 + lane;
     const bool valid = i < n1;
     const int nch = (n2 + kChunk - 1) / kChunk;
     // the slot's fp32 candidate pairs and chunk boxes (wide_prep_kernel), read
@@ -2113,14 +2125,14 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
         uint32_t U = 0x7f800000u;   // +inf: no pruning
         if (ps.screen) {
             if (warm) {
-                const int j0 = pm[lane];
+                const int j0 = pm[gq * 64 + lane];
                 const int j1 = j0 + 1 < n2 ? j0 + 1 : j0 - 1;   // warm implies n2 >= 2
                 const float2 a0 = cf_at(candf, j0), a1 = cf_at(candf, j1);
                 U = valid ? max(__float_as_uint(screen_d32(a0.x, a0.y, fx, fy)),
                                 __float_as_uint(screen_d32(a1.x, a1.y, fx, fy)))
                           : 0u;
             }
-            for (int c = wave; c < nch; c += NW) {
+            for (int c = wg; c < nch; c += NW) {
                 if (warm) {
                     const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, cbox[c]);
                     if (!__builtin_amdgcn_ballot_w64(valid && __float_as_uint(lb) <= U)) continue;   // uniform
@@ -2145,13 +2157,15 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
         xs[(wave * 3 + 2) * 64 + lane] = min(M2, U);   // (every wave holds the same U)
         __syncthreads();
         tstamp(1);
-        if (wave == 0) {
+        double tot = 0.0;
+        if (wave < G) {   // the group leaders
             // merge: the smallest chunk minimum, the lowest chunk on ties (the
             // waves' chunks interleave), and the second smallest over all chunks
             uint32_t m1 = 0xffffffffu, m2 = 0xffffffffu;
             int c1 = 0;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) {
+            for (int w0 = 0; w0 < NW; ++w0) {
+                const int w = gq + G * w0;
                 const uint32_t a1 = xs[(w * 3 + 0) * 64 + lane], a2 = xs[(w * 3 + 2) * 64 + lane];
                 const int ac = static_cast<int>(xs[(w * 3 + 1) * 64 + lane]);
                 c1 = (a1 < m1 || (a1 == m1 && ac < c1)) ? ac : c1;
@@ -2227,7 +2241,7 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
                 }
             }
             tstamp(3);
-            pm[lane] = bi;   // the next iteration's prediction (read after the barrier below)
+            pm[gq * 64 + lane] = bi;   // the next iteration's prediction (read after the barriers below)
             // sums (as icp_kernel step 4), this group's 64 queries
             const double2 c = *reinterpret_cast<const double2*>(pconst + kPcX);
             const double2 gmv = *reinterpret_cast<const double2*>(pconst + kGm1);
@@ -2251,7 +2265,14 @@ __global__ __launch_bounds__(kWideBlock) void icp_wide_kernel(IcpArgs a, const f
                 rsum_add(ay * m.x, gs, acc[10], acc[11]);
                 rsum_add(ay * m.y, gs, acc[12], acc[13]);
             }
-            double tot = wave_sum_exact16(acc);
+            tot = wave_sum_exact16(acc);
+            if (G > 1 && gq == 1 && lane < 16) gsum[lane] = tot;
+        }
+        if constexpr (G > 1) {
+            __syncthreads();   // group 1's sums (exact partials: any order gives the same bits)
+            if (wave == 0 && lane < 16) tot += gsum[lane];
+        }
+        if (wave == 0) {
             tstamp(4);
             bool arrived = true;
             if (parts > 1) tot = gang_exchange_wave(tot, slots, part, parts, it, a.gang_wait, arrived);
@@ -2631,8 +2652,8 @@ constexpr int kAutoShare = SLAM_AUTO_SHARE;
 
 // per device: the side streams and the fork / join events (created once, reused)
 struct SideStream {
-    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr, join3 = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr, join3 = nullptr, join4 = nullptr;
 };
 static SideStream* side_stream(int dev) {
     static SideStream side[64];
@@ -2644,10 +2665,12 @@ static SideStream* side_stream(int dev) {
         if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&e.stream2, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&e.stream3, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&e.stream4, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&e.join2, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e.join3, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e.join3, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.join4, hipEventDisableTiming) != hipSuccess) {
             e.stream = nullptr;
             return nullptr;
         }
@@ -2730,9 +2753,11 @@ static int launch_bulk_gangs(const IcpArgs& args, int B, const BulkGangInstance*
 
 // W pairs (args.order[0..W)) on the wide tier: one workgroup per 64-query
 // group, the parts of a pair on one XCD (slots as launch_gangs).
+static thread_local int g_wide_groups = 1;   // query groups per wide workgroup (2: 16 waves, a CU each)
 static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipStream_t s, uint64_t* slots,
                        float2* wcand, int share) {
-    const int parts = (max_n1 + 63) / 64;
+    const int G = g_wide_groups;
+    const int parts = (max_n1 + 64 * G - 1) / (64 * G);
     if (max_n2 > kCandCap || parts < 1 || parts > kTeamMaxParts) return fail(SLAM_EINVAL, "icp wide tier: shape");
     IcpArgs a = args;
     a.stamps = g_icp_stamps;   // diagnostics: per-part phase cycles (icp_wide_kernel)
@@ -2742,14 +2767,19 @@ static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipSt
     a.n_gangs = W;
     a.gang_slots = slots;
     a.gang_wait = g_gang_wait;
-    const size_t need = wide_lds_bytes(a.cand_cap);
+    const size_t need = wide_lds_bytes(a.cand_cap, G);
     if (need > kMaxLds) return fail(SLAM_EINVAL, "icp wide tier: LDS");
-    const size_t lds = max(need, kMaxLds / static_cast<size_t>(max(share, 1)));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(icp_wide_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds));
+    // two groups per workgroup: 16 waves, one workgroup per CU (share 1)
+    const size_t lds = max(need, kMaxLds / static_cast<size_t>(G > 1 ? 1 : max(share, 1)));
+    const void* fn = G > 1 ? reinterpret_cast<const void*>(icp_wide_kernel<2>) : reinterpret_cast<const void*>(icp_wide_kernel<1>);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     hipLaunchKernelGGL(wide_prep_kernel, dim3(W), dim3(256), 0, s, a, wcand);
-    hipLaunchKernelGGL(icp_wide_kernel, dim3((W + 7) / 8 * 8 * parts), dim3(kWideBlock), lds, s, a,
-                       reinterpret_cast<const float4*>(wcand));
+    if (G > 1)
+        hipLaunchKernelGGL(icp_wide_kernel<2>, dim3((W + 7) / 8 * 8 * parts), dim3(2 * kWideBlock), lds, s, a,
+                           reinterpret_cast<const float4*>(wcand));
+    else
+        hipLaunchKernelGGL(icp_wide_kernel<1>, dim3((W + 7) / 8 * 8 * parts), dim3(kWideBlock), lds, s, a,
+                           reinterpret_cast<const float4*>(wcand));
     return check_launch("icp wide kernel");
 }
 
@@ -3102,17 +3132,19 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                            static_cast<const float*>(nullptr), B, g_angle_thresh, order0, ap_slots,
                            static_cast<int64_t>(ap_slot_words), static_cast<const int32_t*>(nullptr), ap_k, args.init, ap,
                            args.out_iters, mix > 0 ? mix : -1);
-        if (hipEventRecord(side0->fork, s) != hipSuccess || hipStreamWaitEvent(side0->stream3, side0->fork, 0) != hipSuccess)
+        if (hipEventRecord(side0->fork, s) != hipSuccess || hipStreamWaitEvent(side0->stream3, side0->fork, 0) != hipSuccess ||
+            (mix > 0 && hipStreamWaitEvent(side0->stream4, side0->fork, 0) != hipSuccess))
             rc = fail(SLAM_EHIP, "icp scheduler: fork");
         else
             ms = side0->stream3;
         IcpArgs w = args;
         w.order = order0;
         w.take_lt = ap_k;
-        if (rc == 0 && mix > 0) {   // the largest turns on wide workgroups (slots below ap_k[1])
-            IcpArgs wm = w;
+        if (rc == 0 && mix > 0) {   // the largest turns on wide workgroups (slots below ap_k[1]), on
+            IcpArgs wm = w;         // stream4 beside the gangs (joined back before the repair launches)
             wm.take_lt = ap_k + 1;
-            rc = launch_wide(wm, mix, max_n1, max_n2, s, ap_slots, ap_cand, cfg_mix_share);
+            rc = launch_wide(wm, mix, max_n1, max_n2, side0->stream4, ap_slots, ap_cand, cfg_mix_share);
+            if (rc == 0 && hipEventRecord(side0->join4, side0->stream4) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: join");
             w.skip_lt = ap_k + 1;   // the gangs take the slots from there to ap_k[0]
         }
         if (rc == 0)
@@ -3194,7 +3226,8 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 rc = fail(SLAM_EHIP, "icp scheduler: join");
             if (rc == 0 && (hipStreamWaitEvent(s, side->join, 0) != hipSuccess ||
                             hipStreamWaitEvent(s, side->join2, 0) != hipSuccess ||
-                            hipStreamWaitEvent(s, side->join3, 0) != hipSuccess))
+                            hipStreamWaitEvent(s, side->join3, 0) != hipSuccess ||
+                            (mix > 0 && hipStreamWaitEvent(s, side->join4, 0) != hipSuccess)))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
             // (with the pre-tier, stream3 = ms: join3 also joins the phases and the gangs)
             if (rc == 0 && (GW > 0 || bg)) {
@@ -3212,7 +3245,8 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 rc = launch(false, r, ap, max_n1, max_n2, stream);
             }
         } else {
-            if (ms != s && (hipEventRecord(side0->join3, ms) != hipSuccess || hipStreamWaitEvent(s, side0->join3, 0) != hipSuccess))
+            if (ms != s && (hipEventRecord(side0->join3, ms) != hipSuccess || hipStreamWaitEvent(s, side0->join3, 0) != hipSuccess ||
+                            (mix > 0 && hipStreamWaitEvent(s, side0->join4, 0) != hipSuccess)))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
             if (rc == 0) rc = launch(false, a, B, max_n1, max_n2, stream);
             if (rc == 0 && ap) {   // the pre-tier's repair (its pairs are not in phase 2's order)
@@ -3222,9 +3256,13 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             }
         }
     }
-    if (ms != s && rc != 0) {   // an error after the pre-tier's fork: still join the phase stream before the free
+    if (ms != s && rc != 0) {   // an error after the pre-tier's fork: still join the side streams before the free
         (void)hipEventRecord(side0->join3, ms);
         (void)hipStreamWaitEvent(s, side0->join3, 0);
+        if (mix > 0) {
+            (void)hipEventRecord(side0->join4, side0->stream4);
+            (void)hipStreamWaitEvent(s, side0->join4, 0);
+        }
     }
     (void)hipFreeAsync(ws, s);
     return rc;
@@ -3350,6 +3388,11 @@ int slam_icp_set_angle_tier_kind(int kind) {
     if (kind != 0 && kind != 2 && kind != 3) return fail(SLAM_EINVAL, "angle tier kind %d not in {0, 2, 3}", kind);
     g_angle_kind = kind;
     g_sched_auto = 0;
+    return ok();
+}
+int slam_icp_set_wide_groups(int groups) {
+    if (groups != 1 && groups != 2) return fail(SLAM_EINVAL, "wide groups %d not in {1, 2}", groups);
+    g_wide_groups = groups;
     return ok();
 }
 int slam_icp_set_angle_tier_mix(int wide_pairs, int share) {

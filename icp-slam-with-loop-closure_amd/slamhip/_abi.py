@@ -44,6 +44,7 @@ SIGNATURES = {
     "slam_icp_set_schedule_auto": (c_int, [c_int]),
     "slam_icp_set_angle_tier_kind": (c_int, [c_int]),
     "slam_icp_set_angle_tier_mix": (c_int, [c_int, c_int]),
+    "slam_icp_set_wide_groups": (c_int, [c_int]),
     "slam_icp_set_eval_counter": (c_int, [c_ptr]),
     "slam_icp_set_trace": (c_int, [c_ptr]),
     "slam_icp_status": (c_int, [c_ptr]),

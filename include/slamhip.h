@@ -339,6 +339,10 @@ int slam_icp_set_angle_tier_kind(int kind);
  * turning pairs (the largest turns) run on wide workgroups, `share` per CU,
  * the rest on the gangs (0: none).  Bit-identical. */
 int slam_icp_set_angle_tier_mix(int wide_pairs, int share);
+/* Diagnostics: query groups per wide-tier workgroup: 1 (8 waves, `share`
+ * workgroups per CU) or 2 (16 waves, one workgroup per CU; a 1081-point pair
+ * on 9 workgroups).  Bit-identical. */
+int slam_icp_set_wide_groups(int groups);
 /* The scheduler's automatic tier profile by batch size (1, default; DESIGN.md
  * section 6): below 2,048 pairs 24 pre-tier pairs on wide workgroups; 2,048 -
  * 8,192 pairs 96 pre-tier pairs on gangs of 3 plus 64 phase-2 heads, the first

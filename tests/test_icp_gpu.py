@@ -479,18 +479,24 @@ def test_gangs_are_bit_identical(k):
             runs[(gangs, parts)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() == 0
         # the wide tier (brute-force screen over candidate slices), alone and before gangs
-        for wide, share, gangs in ((64, 1, 0), (8, 2, 16), (3, 4, 24)):
+        # (groups 2: two query groups per 16-wave workgroup, one workgroup per CU)
+        for wide, share, gangs, groups in ((64, 1, 0, 1), (8, 2, 16, 1), (3, 4, 24, 1), (24, 1, 0, 2), (64, 2, 8, 2)):
+            assert lib.slam_icp_set_wide_groups(groups) == 0
             assert lib.slam_icp_set_schedule_gangs(gangs, 4) == 0
             assert lib.slam_icp_set_schedule_wide(wide, share) == 0
-            runs[("wide", wide, share, gangs)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100,
-                                                             history=True)
+            runs[("wide", wide, share, gangs, groups)] = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05,
+                                                                     max_iters=100, history=True)
             assert lib.slam_icp_gang_timeouts() == 0
+        assert lib.slam_icp_set_wide_groups(1) == 0
         assert lib.slam_icp_set_schedule_wide(0, 1) == 0
         # the angle pre-tier: the turning pairs on the wide tier from their
         # initial transforms, beside phase 1 of the rest (with gangs, with heads only)
         # (kind 0: wide workgroups; 2 / 3: bulk gangs of that many workgroups)
         for amax, athr, gangs, kind in ((24, 0.3, 24, 0), (64, 0.05, 24, 0), (8, 0.3, 0, 0), (48, 0.3, 24, 3),
-                                        (96, 0.05, 0, 2), (200, 0.05, 24, 3)):
+                                        (96, 0.05, 0, 2), (200, 0.05, 24, 3), (40, 0.05, 0, 20)):
+            # kind 20: the wide pre-tier with two query groups per workgroup
+            assert lib.slam_icp_set_wide_groups(2 if kind == 20 else 1) == 0
+            kind = 0 if kind == 20 else kind
             assert lib.slam_icp_set_schedule_gangs(gangs, 4) == 0
             assert lib.slam_icp_set_angle_tier(amax, athr) == 0
             assert lib.slam_icp_set_angle_tier_kind(kind) == 0
@@ -506,6 +512,7 @@ def test_gangs_are_bit_identical(k):
                                                           history=True)
             assert lib.slam_icp_gang_timeouts() == 0
         assert lib.slam_icp_set_angle_tier_mix(0, 2) == 0
+        assert lib.slam_icp_set_wide_groups(1) == 0
         assert lib.slam_icp_set_angle_tier(*DEFAULT_ANGLE) == 0
         assert lib.slam_icp_set_angle_tier_kind(0) == 0
         # bulk gangs: both phases' bulk as gangs of 2 / 3 ordinary workgroups
@@ -521,6 +528,7 @@ def test_gangs_are_bit_identical(k):
         ro_single = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=7, rotation_only=True)
         assert lib.slam_icp_set_schedule_gangs(1, 1) != 0   # a gang needs two parts
     finally:
+        lib.slam_icp_set_wide_groups(1)
         lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)
         lib.slam_icp_set_schedule_auto(1)
@@ -551,9 +559,12 @@ def test_gang_timeouts_are_repaired(k):
         assert lib.slam_icp_set_schedule(-1, 1024) == 0
         assert lib.slam_icp_set_gang_wait(1) == 0
         lib.slam_icp_gang_timeouts()   # clear
-        for gangs, parts, wide, bulk, angle, kind in ((64, 4, 0, 0, 0, 0), (16, 0, 0, 0, 0, 0), (0, 4, 16, 0, 0, 0),
-                                                      (8, 4, 0, 2, 0, 0), (0, 4, 0, 3, 0, 0), (0, 4, 0, 0, 16, 0),
-                                                      (24, 4, 0, 0, 48, 3)):
+        for gangs, parts, wide, bulk, angle, kind, groups in ((64, 4, 0, 0, 0, 0, 1), (16, 0, 0, 0, 0, 0, 1),
+                                                              (0, 4, 16, 0, 0, 0, 1), (8, 4, 0, 2, 0, 0, 1),
+                                                              (0, 4, 0, 3, 0, 0, 1), (0, 4, 0, 0, 16, 0, 1),
+                                                              (24, 4, 0, 0, 48, 3, 1), (0, 4, 16, 0, 0, 0, 2),
+                                                              (0, 4, 0, 0, 16, 0, 2)):
+            assert lib.slam_icp_set_wide_groups(groups) == 0
             assert lib.slam_icp_set_schedule_gangs(gangs, parts) == 0
             assert lib.slam_icp_set_schedule_wide(wide, 1) == 0
             assert lib.slam_icp_set_bulk_gangs(4096 if bulk else 0, max(bulk, 2)) == 0
@@ -566,6 +577,7 @@ def test_gang_timeouts_are_repaired(k):
             for h0, h1 in zip(single.hist, r.hist):
                 assert np.array_equal(h0, h1), (gangs, parts)
     finally:
+        lib.slam_icp_set_wide_groups(1)
         lib.slam_icp_set_gang_wait(0)
         lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_bulk_gangs(*DEFAULT_BULK)

@@ -13,7 +13,7 @@ prefix of the 10k one.)  GPU only.
 Environment: SHARD_TOTAL (10000 pairs), SHARD_N (2,4,8), SHARD_SEED (2025:
 the C3 stream), SHARD_DROPOUT (0: 1081-point scans; 0.35: ragged 700-1081),
 SHARD_MODE (contiguous | balanced | both: slamhip.dist.contiguous_shards /
-balanced_shards).
+balanced_shards), SHARD_WIDE_GROUPS (query groups per wide-tier workgroup).
 """
 import os
 import sys
@@ -32,6 +32,8 @@ def main():
     from slamhip import icp as k
     lib = _abi.lib()
     settings = sys.argv[1:] or ["auto"]
+    if os.environ.get("SHARD_WIDE_GROUPS"):   # query groups per wide-tier workgroup (1 or 2)
+        assert lib.slam_icp_set_wide_groups(int(os.environ["SHARD_WIDE_GROUPS"])) == 0
     total = int(os.environ.get("SHARD_TOTAL", "10000"))
     seed = int(os.environ.get("SHARD_SEED", "2025"))
     dropout = float(os.environ.get("SHARD_DROPOUT", "0"))

@@ -42,7 +42,7 @@ FLOP_PER_EVAL = 5                 # 2 sub, 2 mul, 1 add per candidate distance
 # issue-bound candidate rate of the exact scan (~8 VALU
 # instructions per candidate): 256 CU x 2.4 GHz x 64 lanes / 8
 ISSUE_BOUND_EVALS_PER_S = 4.9e12
-DEFAULT_SHARD = "contiguous"
+DEFAULT_SHARD = "balanced"
 KERNEL_SOURCES = ("icp-slam-with-loop-closure_amd/csrc/icp_kernels.hip", "icp-slam-with-loop-closure_amd/csrc/common.hpp")
 
 

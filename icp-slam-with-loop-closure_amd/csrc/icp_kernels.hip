@@ -2578,7 +2578,7 @@ static thread_local int g_sched_heads = 64;
 // 3.12 ms without the exchange/head tiers and 3.40 ms with them, the 2,500-pair
 // shard 2.84 vs 2.31 ms, so the tiers start below 4,096 pairs
 #ifndef SLAM_AUTO_ANGLE
-#define SLAM_AUTO_ANGLE 24
+#define SLAM_AUTO_ANGLE 40
 #endif
 #ifndef SLAM_AUTO_SHARE
 #define SLAM_AUTO_SHARE 2
@@ -2635,18 +2635,25 @@ static thread_local int g_angle_mix = 0;
 static thread_local int g_angle_mix_share = 2;
 // Automatic tier profile by batch size (the default; any explicit tier setter
 // turns it off, slam_icp_set_schedule_auto(1) turns it back on), measured on
-// every rank's shard of the 10k C3 stream (tools/shard_sweep.py,
-// profiles/r05_shard_sweep*.txt):
-//   B <  kAutoSmall (8-rank shards): the angle pre-tier, kAutoAngle pairs on
-//        wide workgroups sharing a CU kAutoShare ways, no phase-2 tiers;
-//   B <= kSortOneMax (4- and 2-rank shards): the angle pre-tier as bulk gangs
-//        of 3 (kAutoMidAngle pairs) and, in phase 2, 64 heads, the first 24 as
-//        gangs of 4 (5,000 pairs: 2.55 ms with 96 pre-tier pairs, 2.79 with 48, 3.77
-//        with the heads alone; profiles/r05_shard_sweep11.txt);
+// every rank's shard of the 10k C3 stream and of a second stream (seed 7),
+// contiguous and cost-balanced (tools/shard_sweep.py, profiles/r06_wide_sweep*.txt):
+//   B <  kAutoSmall (8-rank shards): the angle pre-tier, up to kAutoAngle
+//        turning pairs (all of a shard's, in practice) on wide workgroups of
+//        two query groups, one per CU; no phase-2 tiers (round 6: 1,250-pair
+//        shards 1.18-1.19 ms balanced, against 1.55 with 24 pairs two per CU);
+//   B <  kHeadsMaxPairs (4-rank shards): the same with up to kAutoMidWide
+//        pairs (2,500 pairs: 1.91 / 2.10 ms on the two streams, against 2.58 /
+//        3.23 with the gang pre-tier);
+//   B <= kSortOneMax (2-rank shards): the angle pre-tier as bulk gangs of 3
+//        (kAutoMidAngle pairs) and, in phase 2, 64 heads, the first 24 as gangs
+//        of 4 (5,000 pairs: 2.55 ms with 96 pre-tier pairs, 2.79 with 48, 3.77
+//        with the heads alone; profiles/r05_shard_sweep11.txt; the wide pre-tier
+//        there 3.1-3.9 ms: 9 CUs per turning pair starve the bulk);
 //   larger batches: no tiers.
 static thread_local int g_sched_auto = 1;
 constexpr int kAutoSmall = 2048;
 constexpr int kAutoMidAngle = 96;
+constexpr int kAutoMidWide = 64;
 constexpr int kAutoAngle = SLAM_AUTO_ANGLE;
 constexpr int kAutoShare = SLAM_AUTO_SHARE;
 
@@ -2753,10 +2760,10 @@ static int launch_bulk_gangs(const IcpArgs& args, int B, const BulkGangInstance*
 
 // W pairs (args.order[0..W)) on the wide tier: one workgroup per 64-query
 // group, the parts of a pair on one XCD (slots as launch_gangs).
-static thread_local int g_wide_groups = 1;   // query groups per wide workgroup (2: 16 waves, a CU each)
+static thread_local int g_wide_groups = 1;   // explicit settings: query groups per wide workgroup
 static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipStream_t s, uint64_t* slots,
-                       float2* wcand, int share) {
-    const int G = g_wide_groups;
+                       float2* wcand, int share, int groups) {
+    const int G = groups > 1 ? 2 : 1;
     const int parts = (max_n1 + 64 * G - 1) / (64 * G);
     if (max_n2 > kCandCap || parts < 1 || parts > kTeamMaxParts) return fail(SLAM_EINVAL, "icp wide tier: shape");
     IcpArgs a = args;
@@ -3012,7 +3019,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     // the tier profile: explicit settings, or the automatic one by batch size
     int cfg_heads = g_sched_heads, cfg_gangs = g_sched_gangs, cfg_parts = g_sched_gang_parts;
     int cfg_wide = g_sched_wide, cfg_share = g_wide_share, cfg_angle = g_angle_max, cfg_akind = g_angle_kind;
-    int cfg_mix = g_angle_mix, cfg_mix_share = g_angle_mix_share;
+    int cfg_mix = g_angle_mix, cfg_mix_share = g_angle_mix_share, cfg_groups = g_wide_groups;
     int tiers_below = g_tiers_below;
     if (g_sched_auto) {
         cfg_wide = 0;
@@ -3021,11 +3028,18 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         cfg_akind = 0;
         cfg_mix = 0;
         cfg_mix_share = 2;
+        cfg_groups = 1;
         if (B < kAutoSmall) {
             cfg_heads = 0;
             cfg_gangs = 0;
             cfg_angle = kAutoAngle;
             cfg_share = kAutoShare;
+            cfg_groups = 2;
+        } else if (B < kHeadsMaxPairs) {
+            cfg_heads = 0;
+            cfg_gangs = 0;
+            cfg_angle = kAutoMidWide;
+            cfg_groups = 2;
         } else if (B <= kSortOneMax) {
             cfg_heads = 64;
             cfg_gangs = 24;
@@ -3143,13 +3157,13 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         if (rc == 0 && mix > 0) {   // the largest turns on wide workgroups (slots below ap_k[1]), on
             IcpArgs wm = w;         // stream4 beside the gangs (joined back before the repair launches)
             wm.take_lt = ap_k + 1;
-            rc = launch_wide(wm, mix, max_n1, max_n2, side0->stream4, ap_slots, ap_cand, cfg_mix_share);
+            rc = launch_wide(wm, mix, max_n1, max_n2, side0->stream4, ap_slots, ap_cand, cfg_mix_share, cfg_groups);
             if (rc == 0 && hipEventRecord(side0->join4, side0->stream4) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: join");
             w.skip_lt = ap_k + 1;   // the gangs take the slots from there to ap_k[0]
         }
         if (rc == 0)
             rc = apg ? launch_bulk_gangs(w, ap, apg, max_n2, s, ap_slots + ap_mix_words)
-                     : launch_wide(w, ap, max_n1, max_n2, s, ap_slots, ap_cand, cfg_share);
+                     : launch_wide(w, ap, max_n1, max_n2, s, ap_slots, ap_cand, cfg_share, cfg_groups);
         a.order = order0;
         a.skip_lt = ap_k;
     }
@@ -3204,7 +3218,8 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 hipStreamWaitEvent(side->stream3, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
             // the wide tier on its own stream (the gangs must not queue behind it)
-            if (rc == 0 && Wd > 0) rc = launch_wide(a, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand, cfg_share);
+            if (rc == 0 && Wd > 0)
+                rc = launch_wide(a, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand, cfg_share, cfg_groups);
             if (rc == 0 && G > 0) {
                 IcpArgs g = a;
                 g.order = order + Wd;

@@ -462,7 +462,8 @@ def bench_c4(iterations=10, reps=5):
     plan = GnPlan(len(guess), ea, eb)
     plan_s = time.perf_counter() - t0
     s = GaussNewton(guess, ea, eb, tf, plan=plan)
-    s.run(2)   # warm-up
+    s.run(2)   # warm-up: the eager run (kernel attributes)
+    s.run(iterations)   # and the capture of the `iterations`-step graph the timed runs replay
     dts = []
     for _ in range(reps):
         s.poses.copy_(dv.to_dev(guess, np.float64, s.poses.device))

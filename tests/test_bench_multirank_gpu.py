@@ -2,7 +2,7 @@
 torchrun starts 2 ranks of bench.py as a fresh child process — the launcher
 runs before anything in that child touches the GPU — both on cuda:0
 (SLAMHIP_ONE_DEVICE=1) with the gloo exchange, a 400-pair stream split 200 /
-200.  Rank 0's JSON line must carry n_gpus 2, pairs_total 400, every rank's
+200 by the default cost-balanced sharding.  Rank 0's JSON line must carry n_gpus 2, pairs_total 400, every rank's
 shard and kernel time, and green parity on its shard against the CPU
 oracle.  Reference fan-out: /root/reference/scripts/main.py:240-247."""
 import json
@@ -41,4 +41,8 @@ def test_bench_two_ranks_one_gpu():
     pr = out["per_rank"]
     assert pr["pairs"] == [200, 200] and pr["max_shard_pairs"] == 200 and len(pr["kernel_ms"]) == 2
     assert all(k > 0 for k in pr["kernel_ms"])
+    # the default cost-balanced sharding: the gathered edges, un-permuted, hold rank 0's results
+    assert pr["shard"] == "balanced" and pr["all_gather_unpermuted_ok_rank0"] is True
+    assert pr["exchange_timeouts"] == [0, 0] and len(pr["longest_pair_iterations"]) == 2
+    assert out["exchange_timeouts"] == 0
     assert out["parity"]["ok"] and out["parity"]["iters_equal"] and out["parity"]["pairs"] >= 2

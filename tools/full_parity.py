@@ -1,6 +1,7 @@
 """Parity of the benchmarked path over EVERY pair of the C3 stream: the GPU's
 batched ICP (default scheduler; the full 10k batch and EVERY rank's shard at
-2 / 4 / 8 GPUs, which run the angle pre-tier and the exchange / head tiers) against the
+2 / 4 / 8 GPUs, contiguous and cost-balanced (slamhip.dist), which run the
+angle pre-tier and the exchange / head tiers) against the
 CPU oracle (oracle/icp_oracle.py, vectorised NumPy, bit-exact with
 src/icp.py), run on the host cores with joblib.  GPU only; ~2 minutes on 16
 cores.
@@ -57,12 +58,15 @@ def main():
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, n + 1)])
     ss = k.ScanSet(seq.scans)
     from slamhip import dist as sd
-    runs = {"all": (0, k.icp_batch(ss, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=EPS, max_iters=MAX_ITERS))}
-    for nr in (2, 4, 8):   # EVERY rank's shard (the tier profile depends on the shard size)
-        for r in range(nr):
-            lo, hi, _ = sd.shard_range(n, nr, r)
-            runs[f"ranks{nr}_rank{r}"] = (lo, k.icp_batch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi],
-                                                           epsilon=EPS, max_iters=MAX_ITERS))
+    idx_all = np.arange(n)
+    runs = {"all": (idx_all, k.icp_batch(ss, idx_all + 1, idx_all, inits, epsilon=EPS, max_iters=MAX_ITERS))}
+    keys = sd.turn_keys(inits)
+    for mode in ("contiguous", "balanced"):   # both shardings bench.py offers
+        for nr in (2, 4, 8):   # EVERY rank's shard (the tier profile depends on the shard size)
+            shards = sd.balanced_shards(keys, nr) if mode == "balanced" else sd.contiguous_shards(n, nr)
+            for r, idx in enumerate(shards):
+                runs[f"{mode}_ranks{nr}_rank{r}"] = (idx, k.icp_batch(ss, idx + 1, idx, inits[idx], epsilon=EPS,
+                                                                       max_iters=MAX_ITERS))
     from joblib import Parallel, delayed
     t0 = time.perf_counter()
     ref = Parallel(n_jobs=workers, backend="loky", batch_size=16)(
@@ -76,13 +80,12 @@ def main():
     out = {"workload": f"C3 stream seed 2025, {n} consecutive pairs of 1081-point scans, scripts/main.py parameters",
            "oracle": "oracle/icp_oracle.py (vectorised, bit-exact with the reference's src/icp.py)",
            "oracle_seconds": round(dt, 1), "oracle_workers": workers, "runs": {}}
-    for key, (lo, res) in runs.items():
+    for key, (sl, res) in runs.items():
         cnt = len(res.iters)
-        sl = slice(lo, lo + cnt)
         dtf = np.abs(res.tf - rtf[sl]).max(axis=(1, 2))
         derr = np.abs(res.err - rerr[sl]) / np.maximum(1.0, np.abs(rerr[sl]))
         out["runs"][key] = {
-            "pairs": cnt, "first_pair": lo, "iters_equal": int(np.sum(res.iters == rit[sl])),
+            "pairs": cnt, "first_pair": int(sl[0]), "iters_equal": int(np.sum(res.iters == rit[sl])),
             "max_abs_tf_diff": float(dtf.max()), "max_rel_err_diff": float(derr.max()),
             "pairs_over_1e-9": int(np.sum((dtf > 1e-9) | (derr > 1e-9) | (res.iters != rit[sl]))),
             "longest_pair_iters": int(res.iters.max())}

@@ -1,7 +1,7 @@
 """Where a lone team-run (or, with --wide, wide-tier) pair's iteration goes:
 per query group (workgroup), wave 0's s_memtime cycles per phase and
 iteration.  Pairs of the 10k C3 stream.  GPU only.
-    python tools/team_stamps.py [--wide] [pair ...]"""
+    python tools/team_stamps.py [--wide | --wide2] [pair ...]"""
 import os
 import sys
 
@@ -13,8 +13,9 @@ import torch  # noqa: E402
 from slamhip import _abi, se2, synthetic  # noqa: E402
 from slamhip import icp as k  # noqa: E402
 
-wide = "--wide" in sys.argv
-pairs = [int(a) for a in sys.argv[1:] if a != "--wide"] or [1118, 236]
+wide = "--wide" in sys.argv or "--wide2" in sys.argv
+groups = 2 if "--wide2" in sys.argv else 1   # --wide2: two query groups per 16-wave workgroup
+pairs = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or [1118, 236]
 seq = synthetic.make_sequence(10001, seed=2025)
 lib = _abi.lib()
 ss = k.ScanSet(seq.scans[:max(pairs) + 2])
@@ -26,6 +27,7 @@ try:
     if wide:
         lib.slam_icp_set_schedule_gangs(0, 4)
         lib.slam_icp_set_schedule_wide(1, 1)
+        lib.slam_icp_set_wide_groups(groups)
     else:
         lib.slam_icp_set_schedule_gangs(1, 0)
     for p in pairs:
@@ -49,3 +51,5 @@ finally:
     lib.slam_icp_set_schedule(-1, 1024)
     lib.slam_icp_set_schedule_gangs(24, 4)
     lib.slam_icp_set_schedule_wide(0, 1)
+    lib.slam_icp_set_wide_groups(1)
+    lib.slam_icp_set_schedule_auto(1)

@@ -133,6 +133,20 @@ def make_workload(args, world, rank):
     return scans, src, dst, inits[idx], shards
 
 
+def tier_profile(B):
+    """The batch scheduler's automatic tier profile for a batch of B pairs
+    (csrc/icp_kernels.hip launch_batch)."""
+    if B < 1024:
+        return "one launch, one workgroup per pair"
+    if B < 2048:
+        return "two-phase; turning pairs (<= 40) on the wide pre-tier, 2 query groups per CU-exclusive workgroup"
+    if B < 4096:
+        return "two-phase; turning pairs (<= 64) on the wide pre-tier, 2 query groups per CU-exclusive workgroup"
+    if B <= 8192:
+        return "two-phase; turning pairs (<= 96) as gangs of 3; phase 2: 64 CU-exclusive heads, 24 as gangs of 4"
+    return "two-phase scheduler (phase 1: 3 iterations per pair; phase 2 slowest-first), no tiers"
+
+
 def host_cpu():
     """(logical CPUs of the machine, CPUs this process may use, model name)."""
     n_all = os.cpu_count() or 1
@@ -534,7 +548,8 @@ def main():
                    "pairs_per_rank": B, "pairs_total": int(pairs_all), "points_per_scan": int(n1.max()),
                    "mean_icp_iterations": round(iters_all / pairs_all, 3),
                    "kernel_instance": f"{bb.value}x{qq.value}", "parallelism": f"dp{world}",
-                   "sharding": "weak (own stream per rank)" if args.weak else args.shard},
+                   "sharding": "weak (own stream per rank)" if args.weak else args.shard,
+                   "tier_profile": tier_profile(B)},
         "roofline": {
             # achieved = candidate evaluations per second against
             # the VALU issue bound 4.9e12 /s (= 24.5 TFLOP/s at 5 flops each)

@@ -251,6 +251,63 @@ __device__ __forceinline__ bool gj_invert(double* A, double* C) {
     return bad;
 }
 
+// Wide levels (many odd blocks): ONE workgroup per odd block folds the previous
+// level's updates into D_i, inverts it (the same gj_invert) and writes G_i over
+// D_i (an eliminated block's D is not read again); the level's odd kernel then
+// stages G_i (preinv) instead of every one of its 2 ng + mct workgroups
+// inverting D_i again.  The same operations in the same order: bit-identical.
+template <int T>
+__global__ __launch_bounds__(kThreads, 2) void inv_kernel(double* __restrict__ D, const double* __restrict__ SP,
+                                                      const double* __restrict__ SN, int32_t nb, int32_t s,
+                                                      int32_t* __restrict__ status) {
+    using L = Lds<T>;
+    constexpr int WB = L::WB, LDA = L::LDA, PER = T * T;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* A = lds;
+    double* C = A + WB * LDA;
+    const int i = s + 2 * s * blockIdx.x;
+    const int sp = s / 2;
+    const int tid = threadIdx.x;
+    const int64_t B2 = static_cast<int64_t>(WB) * WB;
+    {   // the odd kernel's staging with the fold, verbatim
+        const double* Di = D + i * B2;
+        const double* sn = SN + (i - sp) * B2;
+        const double* spp = SP + (i + sp) * B2;
+        const bool h1 = sp > 0, h2 = sp > 0 && i + sp < nb;
+        double g[PER];
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) g[qq] = Di[tid + kThreads * qq];
+        if (h1) {
+            double a1[PER];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) a1[qq] = sn[tid + kThreads * qq];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) g[qq] -= a1[qq];
+        }
+        if (h2) {
+            double a2[PER];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) a2[qq] = spp[tid + kThreads * qq];
+#pragma unroll
+            for (int qq = 0; qq < PER; ++qq) g[qq] -= a2[qq];
+        }
+#pragma unroll
+        for (int qq = 0; qq < PER; ++qq) {
+            const int e = tid + kThreads * qq;
+            A[(e / WB) * LDA + e % WB] = g[qq];
+        }
+    }
+    __syncthreads();
+    const bool bad = gj_invert<T>(A, C);   // ends with a barrier
+    if (bad && tid == 0) *status = 1;
+    double* Gi = D + i * B2;
+#pragma unroll
+    for (int qq = 0; qq < PER; ++qq) {
+        const int e = tid + kThreads * qq;
+        Gi[e] = A[(e / WB) * LDA + e % WB];
+    }
+}
+
 // Odd blocks of level s: grid (n_odd [+ combine workgroups], 2 ng + 1) with
 // ng = ceil(T / cpw) column-tile groups of cpw tiles (the host picks cpw per
 // level so its workgroups fit the chip).  Every workgroup inverts D_i itself,
@@ -267,7 +324,8 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
                                                       double* __restrict__ SPb, double* __restrict__ SNb, int32_t nb,
                                                       int32_t s, int32_t cpw, int32_t n_odd, int32_t mc,
                                                       int32_t* __restrict__ status, double* __restrict__ bzo,
-                                                      const int32_t* __restrict__ pslot, double* __restrict__ Pw) {
+                                                      const int32_t* __restrict__ pslot, double* __restrict__ Pw,
+                                                      int32_t preinv) {
     using L = Lds<T>;
     constexpr int WB = L::WB, LDA = L::LDA, LDC = L::LDC, K4 = WB / 4;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -328,8 +386,11 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
     // D_i and b_i with the previous level's Schur updates folded in while
     // staging: D_i -= Sn_{i-sp} + Sp_{i+sp} (older levels reached D_i through
     // the combine workgroups of their next level: every block is at most one
-    // level behind, and the subtraction order is the per-level sequence)
-    {
+    // level behind, and the subtraction order is the per-level sequence).
+    // preinv: inv_kernel already folded and inverted D_i in place (G_i).
+    if (preinv) {
+        stage<T>(D + i * B2, A);
+    } else {
         constexpr int PER = T * T;
         const double* Di = D + i * B2;
         const double* sn = SN + (i - sp) * B2;
@@ -396,9 +457,11 @@ __global__ __launch_bounds__(kThreads, 2) void odd_kernel(double* __restrict__ D
     }
     __syncthreads();
     GJ_STAMP(3);
-    const bool bad = gj_invert<T>(A, C);   // A = G (ends with a barrier)
+    if (!preinv) {
+        const bool bad = gj_invert<T>(A, C);   // A = G (ends with a barrier)
+        if (bad && q == 0 && tid == 0) *status = 1;
+    }
     GJ_STAMP(4);
-    if (bad && q == 0 && tid == 0) *status = 1;
     for (int tj = tj0; tj < tj1; ++tj) {
         // first product: column tile tj of X_i = G E_p or Y_i = G E_i^T: the
         // tile of E (the B operand, shared by every output tile) is loaded once,
@@ -1170,6 +1233,11 @@ __global__ __launch_bounds__(kThreads) void border_solve_kernel(const double* __
 }  // namespace bcrgj
 
 constexpr int kBcrGjSlots = 2 * 256;   // odd-kernel workgroups resident at once (2 per CU)
+// odd blocks from which a level inverts them once (inv_kernel; 0 = never, the
+// default: measured in round 6 at C4, splitting level 1 (234 blocks) or levels
+// 1-2 costs 2-4 %: 5,340-5,347 it/s unsplit against 5,240-5,271 / 5,094-5,211,
+// bit-identical chi2; profiles/r06_gn_ab_split.txt)
+constexpr int kGjSplitMin = 0;
 
 BcrGjBufs bcr_gj_bufs(double* work, int32_t nv, int32_t Wb, int32_t mc) {
     const int64_t nb = (nv + Wb - 1) / Wb;
@@ -1208,7 +1276,16 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
     if (sc && (mc > 32 || mc < 16)) return fail(SLAM_EINVAL, "gn: Schur border with %d RHS columns", mc);
     using OddFn = void (*)(double*, const double*, double*, double*, double*, double*, double*, double*,
                            double*, double*, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t*, double*,
-                           const int32_t*, double*);
+                           const int32_t*, double*, int32_t);
+    using InvFn = void (*)(double*, const double*, const double*, int32_t, int32_t, int32_t*);
+    static const InvFn invs[6] = {bcrgj::inv_kernel<1>, bcrgj::inv_kernel<2>, bcrgj::inv_kernel<3>,
+                                  bcrgj::inv_kernel<4>, bcrgj::inv_kernel<5>, bcrgj::inv_kernel<6>};
+    // levels with at least this many odd blocks invert them once (inv_kernel),
+    // before the products (SLAMHIP_GN_SPLIT_MIN=n selects it for A/B; 0 = never)
+    static const int split_min = [] {
+        const char* e = getenv("SLAMHIP_GN_SPLIT_MIN");
+        return e ? atoi(e) : kGjSplitMin;
+    }();
     static const OddFn odds[6] = {bcrgj::odd_kernel<1>, bcrgj::odd_kernel<2>, bcrgj::odd_kernel<3>,
                                   bcrgj::odd_kernel<4>, bcrgj::odd_kernel<5>, bcrgj::odd_kernel<6>};
     static const size_t lds1[6] = {bcrgj::Lds<1>::bytes, bcrgj::Lds<2>::bytes, bcrgj::Lds<3>::bytes,
@@ -1222,9 +1299,12 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
     const size_t* lds = sc ? ldss : mct > 0 ? ldsm : lds1;
     static bool attrs = false;
     if (!attrs) {   // not a stream operation: the launch sequence stays graph-capturable
-        for (int t = 0; t < 6; ++t)
+        for (int t = 0; t < 6; ++t) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(odds[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       static_cast<int>(ldss[t]));
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(invs[t]), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(lds1[t]));
+        }
         attrs = true;
     }
     const int T = Wb / 16;
@@ -1238,12 +1318,14 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
         // (inversion ~42k cycles, X / Y product ~6k, Sp + E' ~11k per column
         // tile) over the rounds of kBcrGjSlots resident workgroups.  (A third
         // workgroup set for E' beside Sp measured slower: 2,530 -> 2,395 it/s.)
+        // (preinv: the inversion runs once per block before, a workgroup only stages G_i)
+        const int preinv = split_min > 0 && n_odd >= split_min ? 1 : 0;
         int cpw = T;
         double best = 1e30;
         for (int c = 1; c <= T; ++c) {
             const int wgs = n_odd * (2 * ((T + c - 1) / c) + max(mct, 1));
             const int rounds = (wgs + kBcrGjSlots - 1) / kBcrGjSlots;
-            const double est = rounds * (42.0 + c * 17.0);
+            const double est = rounds * ((preinv ? 4.0 : 42.0) + c * 17.0);
             if (est < best) {
                 best = est;
                 cpw = c;
@@ -1252,10 +1334,13 @@ int bcr_gj_levels(const BcrGjBufs& b, int32_t nv, int32_t Wb, int32_t mc, int32_
         const int ng = (T + cpw - 1) / cpw;
         // + the combine workgroups of the blocks that stay even (j = 0, 2s, ...)
         const int n_comb = s > 1 ? n_even : 0;
+        if (preinv)
+            hipLaunchKernelGGL(invs[T - 1], dim3(n_odd), dim3(bcrgj::kThreads), lds1[T - 1], st, b.D, b.SP, b.SN, nb, s,
+                               status);
         hipLaunchKernelGGL(odds[T - 1], dim3(n_odd + n_comb, max(2 * ng + max(mct, 1), bcrgj::kCombineSplit)),
                            dim3(bcrgj::kThreads), lds[T - 1], st, b.D, Ec, En, b.Xs, b.Ys, b.SP, b.SN, b.bz, b.SPb,
                            b.SNb, nb, s, cpw, n_odd, mc, status, sc ? b.bzo : nullptr, sc ? sc->pslot : nullptr,
-                           sc ? sc->P : nullptr);
+                           sc ? sc->P : nullptr, preinv);
         last = s;
     }
     // block 0 (always even): the last level's Sp, then x_0

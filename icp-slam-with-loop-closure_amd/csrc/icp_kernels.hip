@@ -1930,6 +1930,12 @@ __host__ __device__ constexpr size_t wide_lds_bytes(int cap, int groups = 1) {
            static_cast<size_t>(kWideWaves * groups) * 3 * 64 * sizeof(uint32_t) + 24 * sizeof(double) +
            static_cast<size_t>(groups) * 64 * sizeof(int32_t);
 }
+// The wide tier's pruning bound: the runner-up over this many candidates around
+// a query's last match
+#ifndef SLAM_WIDE_UWIN
+#define SLAM_WIDE_UWIN 5   // round 6: lone pair 21.4k -> 18.0k cycles per iteration against 2 (profiles/r06_wide_stamps5.txt)
+#endif
+constexpr int kUWin = SLAM_WIDE_UWIN;
 // A wide slot's global slab (float4 units): the fp32 candidate pairs (cap / 2),
 // then one bounding box per chunk of kChunk candidates (cap / kChunk)
 __host__ __device__ constexpr int64_t wide_slab_f4(int cap) { return cap / 2 + cap / kChunk; }
@@ -2088,9 +2094,9 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
     // the few chunks a group's queries need spread over the waves)
     const float4* __restrict__ cg = wcand + static_cast<int64_t>(slot) * wide_slab_f4(cap);
     const float4* __restrict__ cbox = cg + cap / 2;
-    // pruning (round 6): from the second iteration of a launch on, a lane's last
-    // match j0 and its neighbour bound the runner-up: U = max(d32(j0), d32(j0 +- 1))
-    // >= M2 >= M1, so a chunk whose box lies farther than U from the lane's
+    // pruning (round 6): from the second iteration of a launch on, the kUWin
+    // candidates around a lane's last match bound the runner-up: U = the second
+    // smallest of their screened distances >= M2 >= M1, so a chunk whose box lies farther than U from the lane's
     // query holds neither the minimum nor the runner-up; it is skipped when no
     // lane of the wave needs it.  The certification takes min(M2, U) as its
     // bound on the other candidates (skipped ones are > U): results unchanged.
@@ -2125,18 +2131,44 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
         uint32_t U = 0x7f800000u;   // +inf: no pruning
         if (ps.screen) {
             if (warm) {
-                const int j0 = pm[gq * 64 + lane];
-                const int j1 = j0 + 1 < n2 ? j0 + 1 : j0 - 1;   // warm implies n2 >= 2
-                const float2 a0 = cf_at(candf, j0), a1 = cf_at(candf, j1);
-                U = valid ? max(__float_as_uint(screen_d32(a0.x, a0.y, fx, fy)),
-                                __float_as_uint(screen_d32(a1.x, a1.y, fx, fy)))
-                          : 0u;
+                // the second smallest screened distance over kUWin consecutive
+                // candidates around the last match (distinct: warm implies n2 >= kUWin)
+                const int jb = min(max(pm[gq * 64 + lane] - kUWin / 2, 0), n2 - kUWin);
+                uint32_t u1 = 0xffffffffu, u2 = 0xffffffffu;
+#pragma unroll
+                for (int q = 0; q < kUWin; ++q) {
+                    const float2 aq = cf_at(candf, jb + q);
+                    take_key(__float_as_uint(screen_d32(aq.x, aq.y, fx, fy)), u1, u2);
+                }
+                U = valid ? u2 : 0u;
             }
+#ifndef SLAM_WIDE_NO_BOXPF
+            // the chunks this wave needs, as a mask over its chunks wg + NW k: the
+            // box reads (scalar loads, uniform) four at a time, then the tests
+            uint32_t needm = 0xffffffffu;
+            if (warm) {
+                needm = 0u;
+                for (int k0 = 0; wg + NW * k0 < nch; k0 += 4) {
+                    float4 bq[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) bq[u] = cbox[min(wg + NW * (k0 + u), nch - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, bq[u]);
+                        const bool any = __builtin_amdgcn_ballot_w64(valid && __float_as_uint(lb) <= U) != 0;
+                        needm |= (any && wg + NW * (k0 + u) < nch ? 1u : 0u) << (k0 + u);
+                    }
+                }
+            }
+            for (int c = wg, k = 0; c < nch; c += NW, ++k) {
+                if (!((needm >> k) & 1u)) continue;   // uniform
+#else
             for (int c = wg; c < nch; c += NW) {
                 if (warm) {
                     const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, cbox[c]);
                     if (!__builtin_amdgcn_ballot_w64(valid && __float_as_uint(lb) <= U)) continue;   // uniform
                 }
+#endif
                 const float4* cp = cg + c * (kChunk / 2);
                 uint32_t cm = 0xffffffffu;
 #pragma unroll
@@ -2323,7 +2355,7 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
         }
         T.m00 = uniform_d(tb[0]); T.m01 = uniform_d(tb[1]); T.m02 = uniform_d(tb[2]);
         T.m10 = uniform_d(tb[3]); T.m11 = uniform_d(tb[4]); T.m12 = uniform_d(tb[5]);
-        warm = n2 >= 2;
+        warm = n2 >= kUWin;
     }
 }
 

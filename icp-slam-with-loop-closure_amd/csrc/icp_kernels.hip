@@ -1933,7 +1933,8 @@ __host__ __device__ constexpr size_t wide_lds_bytes(int cap, int groups = 1) {
 // The wide tier's pruning bound: the runner-up over this many candidates around
 // a query's last match
 #ifndef SLAM_WIDE_UWIN
-#define SLAM_WIDE_UWIN 5   // round 6: lone pair 21.4k -> 18.0k cycles per iteration against 2 (profiles/r06_wide_stamps5.txt)
+#define SLAM_WIDE_UWIN 5   // round 6: lone pair 21.4k -> 18.0k cycles per iteration against 2, 9: 19.1k
+                           // (profiles/r06_wide_stamps5.txt, r06_wide_stamps6.txt)
 #endif
 constexpr int kUWin = SLAM_WIDE_UWIN;
 // A wide slot's global slab (float4 units): the fp32 candidate pairs (cap / 2),
@@ -2142,33 +2143,11 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
                 }
                 U = valid ? u2 : 0u;
             }
-#ifndef SLAM_WIDE_NO_BOXPF
-            // the chunks this wave needs, as a mask over its chunks wg + NW k: the
-            // box reads (scalar loads, uniform) four at a time, then the tests
-            uint32_t needm = 0xffffffffu;
-            if (warm) {
-                needm = 0u;
-                for (int k0 = 0; wg + NW * k0 < nch; k0 += 4) {
-                    float4 bq[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) bq[u] = cbox[min(wg + NW * (k0 + u), nch - 1)];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, bq[u]);
-                        const bool any = __builtin_amdgcn_ballot_w64(valid && __float_as_uint(lb) <= U) != 0;
-                        needm |= (any && wg + NW * (k0 + u) < nch ? 1u : 0u) << (k0 + u);
-                    }
-                }
-            }
-            for (int c = wg, k = 0; c < nch; c += NW, ++k) {
-                if (!((needm >> k) & 1u)) continue;   // uniform
-#else
             for (int c = wg; c < nch; c += NW) {
                 if (warm) {
                     const float lb = box_lb(f32x2{fx, fy}, f32x2{fx, fy}, cbox[c]);
                     if (!__builtin_amdgcn_ballot_w64(valid && __float_as_uint(lb) <= U)) continue;   // uniform
                 }
-#endif
                 const float4* cp = cg + c * (kChunk / 2);
                 uint32_t cm = 0xffffffffu;
 #pragma unroll

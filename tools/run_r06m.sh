@@ -1,0 +1,7 @@
+set -e
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/r06_gpu_tests_m.txt 2>&1
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r06_smoke_m.txt 2>&1
+timeout -k 10 600 python -u tools/full_parity.py 10000 16 > gpurun_out/r06_full_parity.json 2> gpurun_out/r06_full_parity.err
+bash tools/gpu_profile.sh r06b > gpurun_out/r06b_gpu_profile.log 2>&1
+timeout -k 10 400 python -u bench.py > gpurun_out/r06_bench_b.json 2> gpurun_out/r06_bench_b.err

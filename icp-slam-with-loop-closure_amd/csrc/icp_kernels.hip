@@ -708,7 +708,11 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
 // return the total of value q in lane q < 16.  Called by ONE wave per part.
 __device__ __forceinline__ double gang_exchange_wave(double t, uint64_t* slots, int part, int parts, int e,
                                                      uint32_t wait, bool& arrived) {
-    const int lane = threadIdx.x & 63;
+    // an opaque lane index: the sweep's addresses are recomputed at every
+    // exchange (a few VALU) instead of hoisted out of the ICP loop, where the
+    // 16-wave wide instance (128 VGPRs) spilled them to scratch
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
     const uint64_t tag = static_cast<uint64_t>(e + 1) << 32;
     uint64_t* buf = slots + (e & 1) * parts * 32;
     const uint64_t tb = static_cast<uint64_t>(__double_as_longlong(__shfl(t, lane & 15, 64)));
@@ -2190,17 +2194,23 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
             int j1 = c1 * kChunk;
             {
                 const float4* cp = reinterpret_cast<const float4*>(candf + c1 * kChunk);
-                float4 pp[kChunk / 2];
-#pragma unroll
-                for (int t = 0; t < kChunk / 2; ++t) pp[t] = cp[t];
                 float e1[2] = {INFINITY, INFINITY}, e2[2] = {INFINITY, INFINITY};
                 int ej[2] = {0, 0};
+                // (four candidate pairs in flight at a time: 16 VGPRs, not 64 — the
+                // 16-wave instance must fit 128 without spilling)
 #pragma unroll
-                for (int t = 0; t < kChunk / 2; ++t) {
-                    const f32x2v d = screen_pair(pp[t], fx, fy);
-                    const int h = t & 1;
-                    take_cand(d.x, 2 * t, e1[h], e2[h], ej[h]);
-                    take_cand(d.y, 2 * t + 1, e1[h], e2[h], ej[h]);
+                for (int t0 = 0; t0 < kChunk / 2; t0 += 4) {
+                    float4 pp[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pp[u] = cp[t0 + u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = t0 + u;
+                        const f32x2v d = screen_pair(pp[u], fx, fy);
+                        const int h = t & 1;
+                        take_cand(d.x, 2 * t, e1[h], e2[h], ej[h]);
+                        take_cand(d.y, 2 * t + 1, e1[h], e2[h], ej[h]);
+                    }
                 }
                 // chain 0 holds offsets {0,1,4,5,...}, chain 1 {2,3,6,7,...}: on a tie
                 // the smaller offset wins (the full scan's first index)

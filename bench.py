@@ -143,7 +143,7 @@ def tier_profile(B):
     if B < 4096:
         return "two-phase; turning pairs (<= 64) on the wide pre-tier, 2 query groups per CU-exclusive workgroup"
     if B <= 8192:
-        return "two-phase; turning pairs (<= 96) as gangs of 3; phase 2: 64 CU-exclusive heads, 24 as gangs of 4"
+        return "two-phase; turning pairs (<= 96) as gangs of 4; phase 2: 64 CU-exclusive heads, 24 as gangs of 4"
     return "two-phase scheduler (phase 1: 3 iterations per pair; phase 2 slowest-first), no tiers"
 
 

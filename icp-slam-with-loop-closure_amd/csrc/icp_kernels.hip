@@ -2429,6 +2429,9 @@ static const BulkGangInstance kBulkGangInstances[] = {
     {2, 256, 3, icp_kernel<256, 3, false, true, true, kWpe, false, true>},
     {3, 128, 3, icp_kernel<128, 3, false, true, true, kWpe, false, true>},
     {3, 192, 2, icp_kernel<192, 2, false, true, true, kWpe, false, true>},
+    // round 6: gangs of 4 / 6 for the angle pre-tier (slam_icp_set_angle_tier_kind)
+    {4, 192, 2, icp_kernel<192, 2, false, true, true, kWpe, false, true>},
+    {6, 192, 1, icp_kernel<192, 1, false, true, true, kWpe, false, true>},
 };
 static const BulkGangInstance* pick_bulk_gang_instance(int max_n1, int parts) {
     const int groups = (max_n1 + 63) / 64;
@@ -2665,11 +2668,13 @@ static thread_local int g_angle_mix_share = 2;
 //   B <  kHeadsMaxPairs (4-rank shards): the same with up to kAutoMidWide
 //        pairs (2,500 pairs: 1.91 / 2.10 ms on the two streams, against 2.58 /
 //        3.23 with the gang pre-tier);
-//   B <= kSortOneMax (2-rank shards): the angle pre-tier as bulk gangs of 3
-//        (kAutoMidAngle pairs) and, in phase 2, 64 heads, the first 24 as gangs
-//        of 4 (5,000 pairs: 2.55 ms with 96 pre-tier pairs, 2.79 with 48, 3.77
-//        with the heads alone; profiles/r05_shard_sweep11.txt; the wide pre-tier
-//        there 3.1-3.9 ms: 9 CUs per turning pair starve the bulk);
+//   B <= kSortOneMax (2-rank shards): the angle pre-tier as bulk gangs of 4
+//        (kAutoMidAngle pairs; round 6: 2.57 / 2.84 ms on seeds 2025 / 7
+//        against 2.61 / 3.27 with gangs of 3, gangs of 6 2.64 / 2.92,
+//        profiles/r06_gangk_sweep.txt) and, in phase 2, 64 heads, the first 24
+//        as gangs of 4 (round 5: 96 pre-tier pairs 2.55 ms, 48 2.79, the heads
+//        alone 3.77, profiles/r05_shard_sweep11.txt; the wide pre-tier there
+//        3.1-3.9 ms: 9 CUs per turning pair starve the bulk);
 //   larger batches: no tiers.
 static thread_local int g_sched_auto = 1;
 constexpr int kAutoSmall = 2048;
@@ -3065,7 +3070,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             cfg_heads = 64;
             cfg_gangs = 24;
             cfg_angle = kAutoMidAngle;
-            cfg_akind = 3;
+            cfg_akind = 4;
             tiers_below = kSortOneMax + 1;
         } else {
             cfg_heads = 0;
@@ -3120,7 +3125,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const size_t cand_cap_w = static_cast<size_t>(((max(max_n2, 1) + kChunk - 1) / kChunk) * kChunk);
     // (a mixed pre-tier: the wide part's slots first, then the gangs' by slot index)
     const size_t ap_mix_words = static_cast<size_t>(mix) * 2 * wide_parts * 32;
-    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * max(wide_parts, 3) * 32 + ap_mix_words;
+    const size_t ap_slot_words = static_cast<size_t>(ap) * 2 * max(wide_parts, max(cfg_akind, 3)) * 32 + ap_mix_words;
     const size_t ap_bytes = ap ? ((nb + 2) * sizeof(int32_t) + 255) / 256 * 256 + ap_slot_words * sizeof(uint64_t) +
                                      static_cast<size_t>(ap) * wide_slab_f4(static_cast<int>(cand_cap_w)) * sizeof(float4)
                                : 0;
@@ -3421,7 +3426,8 @@ int slam_icp_set_angle_tier(int max_pairs, float thresh_rad) {
 // The angle pre-tier's kind: 0 the wide tier, 2 / 3 bulk gangs of that many
 // ordinary workgroups per pair.
 int slam_icp_set_angle_tier_kind(int kind) {
-    if (kind != 0 && kind != 2 && kind != 3) return fail(SLAM_EINVAL, "angle tier kind %d not in {0, 2, 3}", kind);
+    if (kind != 0 && kind != 2 && kind != 3 && kind != 4 && kind != 6)
+        return fail(SLAM_EINVAL, "angle tier kind %d not in {0, 2, 3, 4, 6}", kind);
     g_angle_kind = kind;
     g_sched_auto = 0;
     return ok();

@@ -332,8 +332,8 @@ int slam_icp_set_tier_limit(int pairs);
  * beside the two-phase schedule of the others (0: off).  Results are
  * bit-identical. */
 int slam_icp_set_angle_tier(int max_pairs, float thresh_rad);
-/* Diagnostics: the angle pre-tier's kind, 0 the wide tier, 2 / 3 bulk gangs
- * of that many ordinary workgroups per pair. */
+/* Diagnostics: the angle pre-tier's kind, 0 the wide tier, 2 / 3 / 4 / 6 bulk
+ * gangs of that many ordinary workgroups per pair. */
 int slam_icp_set_angle_tier_kind(int kind);
 /* Diagnostics: with a gang pre-tier (kind 2 / 3), its first wide_pairs
  * turning pairs (the largest turns) run on wide workgroups, `share` per CU,
@@ -344,10 +344,11 @@ int slam_icp_set_angle_tier_mix(int wide_pairs, int share);
  * on 9 workgroups).  Bit-identical. */
 int slam_icp_set_wide_groups(int groups);
 /* The scheduler's automatic tier profile by batch size (1, default; DESIGN.md
- * section 6): below 2,048 pairs 24 pre-tier pairs on wide workgroups; 2,048 -
- * 8,192 pairs 96 pre-tier pairs on gangs of 3 plus 64 phase-2 heads, the first
- * 24 as gangs of 4; larger batches no tiers.  0: the explicit settings; any of
- * the tier setters above selects them, 1 restores their defaults too. */
+ * section 6): below 2,048 pairs up to 40 turning pre-tier pairs, below 4,096
+ * up to 64, on wide workgroups of two query groups (one per CU); 4,096 - 8,192
+ * pairs up to 96 pre-tier pairs on gangs of 4 plus 64 phase-2 heads, the
+ * first 24 as gangs of 4; larger batches no tiers.  0: the explicit settings;
+ * any of the tier setters above selects them, 1 restores their defaults too. */
 int slam_icp_set_schedule_auto(int on);
 /* Diagnostics: the XCD-aware pair map of launches in stream order: runs of
  * `run` consecutive pairs per XCD (default 16, so consecutive pairs share

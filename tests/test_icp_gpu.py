@@ -493,7 +493,8 @@ def test_gangs_are_bit_identical(k):
         # initial transforms, beside phase 1 of the rest (with gangs, with heads only)
         # (kind 0: wide workgroups; 2 / 3: bulk gangs of that many workgroups)
         for amax, athr, gangs, kind in ((24, 0.3, 24, 0), (64, 0.05, 24, 0), (8, 0.3, 0, 0), (48, 0.3, 24, 3),
-                                        (96, 0.05, 0, 2), (200, 0.05, 24, 3), (40, 0.05, 0, 20)):
+                                        (96, 0.05, 0, 2), (200, 0.05, 24, 3), (40, 0.05, 0, 20), (64, 0.05, 24, 4),
+                                        (64, 0.05, 0, 6)):
             # kind 20: the wide pre-tier with two query groups per workgroup
             assert lib.slam_icp_set_wide_groups(2 if kind == 20 else 1) == 0
             kind = 0 if kind == 20 else kind

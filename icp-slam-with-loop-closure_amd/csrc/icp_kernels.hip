@@ -90,6 +90,7 @@ struct IcpArgs {
     int32_t n_gangs;
     uint64_t* gang_slots;    // [n_gangs][2][gang][32] tagged granules, zeroed before the launch
     uint32_t gang_wait;      // longest wait for the partners of one exchange (s_memrealtime ticks)
+    uint32_t gang_wait_first;   // the same for a launch's FIRST exchange of a pair (partners not resident)
     // PRUNE kernels, scheduler phases: a paused pair's search state (per query
     // i: last match and clearance word at qsave[b * qsave_stride + i]; the
     // motion T_next - T and its slack at dtsave[b * 8 + ..]) so that its resumed
@@ -644,6 +645,14 @@ __device__ __forceinline__ bool certify(double d1, double s2, double a) {
     return s2 > fc;
 }
 
+// A part that gives up on an exchange (timeout, or a partner's abort) writes
+// granules with this tag into its slots of this exchange and of the next: a
+// partner still sweeping this one, one that starts late, or one that got past
+// it (every granule had arrived) stops at once instead of waiting out its own
+// timeout, and the pair goes to the repair launch (tags of real exchanges are
+// e + 1 < 2^31).  A pair that finished at this exchange had its results
+// written by part 0 already; the repair skips it.
+constexpr uint32_t kGangAbortTag = 0xffffffffu;
 // One lane's share of a gang exchange sweep: granule g of parts pp, pp + 2, ...
 // (N per lane, addresses clamped so every load is issued unconditionally),
 // repeated until every tag matches; then the doubles reassembled across the
@@ -662,14 +671,19 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
         for (int k = 0; k < N; ++k)
             x[k] = __hip_atomic_load(buf + min(pp + 2 * k, parts - 1) * 32 + g, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
-        bool ok = true;
+        bool ok = true, ab = false;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const int p = pp + 2 * k;
             v[k] = p == part ? own : static_cast<uint32_t>(x[k]);
             ok &= p >= parts || p == part || (x[k] & 0xffffffff00000000ull) == tag;
+            ab |= p < parts && p != part && (x[k] >> 32) == kGangAbortTag;
         }
         if (__all(ok)) break;
+        if (__any(ab)) {   // a partner gave up (gang_exchange_wave): so does this part, at once
+            arrived = false;
+            break;
+        }
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > wait) {   // a partner never arrived
             if (lane == 0) atomicAdd(&g_gang_timeout, 1);
@@ -732,6 +746,10 @@ __device__ __forceinline__ double gang_exchange_wave(double t, uint64_t* slots, 
         s = gang_sweep<8>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
     else
         s = gang_sweep<kGangSweep / 2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+    if (!arrived) {   // (uniform) tell the partners: at this exchange and at the next (lanes 0-31 / 32-63)
+        __hip_atomic_store(slots + ((e + (lane >> 5)) & 1) * parts * 32 + part * 32 + (lane & 31),
+                           static_cast<uint64_t>(kGangAbortTag) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return s + __shfl_xor(s, 32, 64);   // parts of even + odd index (the same bits in both halves)
 }
 
@@ -1322,7 +1340,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             // a partner that never arrived: stop at once, write nothing (the
             // repair launch re-runs the pair from its phase-1 state)
             if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
-                                            parts, it, a.gang_wait, pconst + kBcast))
+                                            parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, pconst + kBcast))
                 return;
         }
         // The update is the same for every wave: wave 0 computes it and hands the
@@ -1825,7 +1843,7 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
             tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
             tstamp(7);
             if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
-                                            parts, it, a.gang_wait, pconst + kBcast)) {
+                                            parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, pconst + kBcast)) {
                 tflush();
                 return;   // a partner timed out: nothing written, the repair launch re-runs the pair
             }
@@ -2296,7 +2314,8 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
         if (wave == 0) {
             tstamp(4);
             bool arrived = true;
-            if (parts > 1) tot = gang_exchange_wave(tot, slots, part, parts, it, a.gang_wait, arrived);
+            if (parts > 1)
+                tot = gang_exchange_wave(tot, slots, part, parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, arrived);
             tstamp(5);
             double flag = 0.0;
             if (!arrived) {
@@ -2628,6 +2647,13 @@ static const Instance* pick_head_instance(int max_n1) {
 static thread_local int g_sched_gangs = 24;
 static thread_local int g_sched_gang_parts = 4;
 static thread_local uint32_t g_gang_wait = kGangWaitTicks;   // diagnostics can shorten it to force timeouts
+// A pair's first exchange in a launch waits at most this long: a partner that
+// is not resident by then (CUs held by another process, or a shard whose
+// exchange tiers outnumber the CUs for that long) makes the pair give up at
+// once and the repair launch run it on one workgroup — a stall of milliseconds,
+// not the 0.2 s of a later exchange (where every partner has been seen)
+constexpr uint32_t kGangWaitFirstTicks = 400000;   // 4 ms
+static thread_local uint32_t g_gang_wait_first = kGangWaitFirstTicks;
 // Wide tier: the top g_sched_wide keyed pairs of a batch below kHeadsMaxPairs
 // run on icp_wide_kernel, one workgroup per 64-query group, each requesting
 // kMaxLds / g_wide_share of LDS (1: CU-exclusive)
@@ -2727,6 +2753,7 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
         a.n_gangs = G;
         a.gang_slots = slots;
         a.gang_wait = g_gang_wait;
+    a.gang_wait_first = min(g_gang_wait, g_gang_wait_first);
         const size_t lds_need = red_doubles(kTeamBlock) * sizeof(double) +
                                 static_cast<size_t>(a.cand_cap) * (sizeof(double2) + sizeof(float2)) +
                                 static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) + team_xbuf_words() * sizeof(uint32_t);
@@ -2747,6 +2774,7 @@ static int launch_gangs(const IcpArgs& args, int G, int parts, bool team, int ma
     a.n_gangs = G;
     a.gang_slots = slots;
     a.gang_wait = g_gang_wait;
+    a.gang_wait_first = min(g_gang_wait, g_gang_wait_first);
     const size_t lds_need = red_doubles(gi->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2) +
                             static_cast<size_t>(a.cand_cap) * sizeof(float2) +
                             static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
@@ -2773,6 +2801,7 @@ static int launch_bulk_gangs(const IcpArgs& args, int B, const BulkGangInstance*
     a.n_gangs = B;
     a.gang_slots = slots;
     a.gang_wait = g_gang_wait;
+    a.gang_wait_first = min(g_gang_wait, g_gang_wait_first);
     const size_t lds = red_doubles(bg->block) * sizeof(double) + static_cast<size_t>(a.cand_cap) * sizeof(double2) +
                        static_cast<size_t>(a.cand_cap) * sizeof(float2) +
                        static_cast<size_t>(a.cand_cap / kSub) * sizeof(float4) +
@@ -2800,6 +2829,7 @@ static int launch_wide(const IcpArgs& args, int W, int max_n1, int max_n2, hipSt
     a.n_gangs = W;
     a.gang_slots = slots;
     a.gang_wait = g_gang_wait;
+    a.gang_wait_first = min(g_gang_wait, g_gang_wait_first);
     const size_t need = wide_lds_bytes(a.cand_cap, G);
     if (need > kMaxLds) return fail(SLAM_EINVAL, "icp wide tier: LDS");
     // two groups per workgroup: 16 waves, one workgroup per CU (share 1)
@@ -3480,6 +3510,35 @@ int slam_icp_gang_timeouts(void) {
 // Diagnostics: the longest wait of a gang exchange for its partners, in
 // s_memrealtime ticks (100 MHz); 0 restores the default (0.2 s).  Tiny values
 // force timeouts (the repair path).
+int slam_icp_set_gang_first_wait(uint32_t ticks) {
+    g_gang_wait_first = ticks ? ticks : kGangWaitFirstTicks;
+    return ok();
+}
+// Diagnostics: `workgroups` workgroups that each hold a whole CU's LDS and spin
+// for `ticks` of s_memrealtime (bounded), on `stream`: a stand-in for another
+// process occupying CUs (tests/test_icp_gpu.py::test_occupied_cus_cost_milliseconds)
+__global__ __launch_bounds__(64) void occupy_kernel(uint32_t ticks, unsigned long long* sink) {
+    extern __shared__ double lds_occ[];
+    if (threadIdx.x == 0) {
+        lds_occ[0] = 1.0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long n = 0;
+        while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+            __builtin_amdgcn_s_sleep(8);
+            ++n;
+        }
+        if (n == 0 && sink) sink[blockIdx.x] = static_cast<unsigned long long>(lds_occ[0]);
+    }
+}
+int slam_icp_diag_occupy(int workgroups, uint32_t ticks, void* stream) {
+    if (workgroups < 1 || workgroups > 4096 || ticks > 100000000u)
+        return fail(SLAM_EINVAL, "occupy: %d workgroups, %u ticks (at most 1 s)", workgroups, ticks);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(occupy_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(kMaxLds));
+    hipLaunchKernelGGL(occupy_kernel, dim3(workgroups), dim3(64), kMaxLds, as_stream(stream), ticks,
+                       static_cast<unsigned long long*>(nullptr));
+    return check_launch("occupy kernel");
+}
 int slam_icp_set_gang_wait(uint32_t ticks) {
     g_gang_wait = ticks ? ticks : kGangWaitTicks;
     return ok();

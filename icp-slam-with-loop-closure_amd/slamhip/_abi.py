@@ -33,6 +33,8 @@ SIGNATURES = {
     "slam_icp_set_schedule_gangs": (c_int, [c_int, c_int]),
     "slam_icp_gang_timeouts": (c_int, []),
     "slam_icp_set_gang_wait": (c_int, [ctypes.c_uint32]),
+    "slam_icp_set_gang_first_wait": (c_int, [ctypes.c_uint32]),
+    "slam_icp_diag_occupy": (c_int, [c_int, ctypes.c_uint32, c_ptr]),
     "slam_icp_set_schedule_wide": (c_int, [c_int, c_int]),
     "slam_icp_set_bulk_gangs": (c_int, [c_int, c_int]),
     "slam_icp_set_schedule_warm": (c_int, [c_int]),

@@ -304,16 +304,26 @@ int slam_icp_set_bulk_gangs(int below_pairs, int parts);
  * iteration starts warm (1; a transient workspace of 8 B per query — measured
  * no faster on C3, round 4); 0 (default) resumes cold.  Results are identical. */
 int slam_icp_set_schedule_warm(int on);
-/* Gang parts that waited longer than the gang wait (default 0.2 s) for a
- * partner since the last call (read-and-clear; synchronises the device).  Such
- * a part stops at once without writing; after phase 2 the scheduler re-runs
- * every gang pair that did not finish on one workgroup from its saved phase-1
- * state, so the results stay valid (and bit-identical): this count is a
- * warning, not an error.  Scheduler order is a stable sort (deterministic). */
+/* Gang parts that waited longer than the gang wait for a partner since the
+ * last call (read-and-clear; synchronises the device): 4 ms at a pair's first
+ * exchange of a launch (a partner that is not resident by then, e.g. CUs held
+ * by another process), 0.2 s later on.  Such a part stops at once without
+ * writing and marks its next exchange so that partners already past this one
+ * stop there too; after phase 2 the scheduler re-runs every exchange-tier pair
+ * that did not finish on one workgroup from its saved state, so the results
+ * stay valid (and bit-identical): this count is a warning, not an error.
+ * Scheduler order is a stable sort (deterministic). */
 int slam_icp_gang_timeouts(void);
 /* Diagnostics: the gang wait in s_memrealtime ticks (100 MHz); 0 = default.
- * Tiny values force timeouts, exercising the repair path. */
+ * Tiny values force timeouts, exercising the repair path (the first
+ * exchange's wait is the smaller of this and slam_icp_set_gang_first_wait's). */
 int slam_icp_set_gang_wait(uint32_t ticks);
+/* Diagnostics: the first exchange's wait in ticks; 0 = default (4 ms). */
+int slam_icp_set_gang_first_wait(uint32_t ticks);
+/* Diagnostics: `workgroups` workgroups that each hold a whole CU's LDS and
+ * spin for `ticks` (<= 1 s) on `stream` — a stand-in for another process
+ * occupying CUs while a batch runs. */
+int slam_icp_diag_occupy(int workgroups, uint32_t ticks, void* stream);
 /* Diagnostics: phase 2's visiting order of B pairs from their phase-1
  * out_iters (> 0: finished) and keys (last |dE|), by the scheduler's stable
  * bucket sort (device arrays; order[] receives B pair indices). */

@@ -586,6 +586,71 @@ def test_gang_timeouts_are_repaired(k):
     assert lib.slam_icp_gang_timeouts() == 0
 
 
+_OCCUPIER = """
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import torch
+from slamhip import _abi
+torch.cuda.set_device(0)
+lib = _abi.lib()
+assert lib.slam_icp_diag_occupy(int(sys.argv[2]), int(sys.argv[3]), None) == 0
+print("launched", flush=True)
+torch.cuda.synchronize()
+print("done", flush=True)
+"""
+
+
+def test_occupied_cus_do_not_stall_the_exchange_tiers(k):
+    """Another PROCESS holding all but 32 CUs (one CU-exclusive workgroup each)
+    for 0.6 s while an 8-rank-size shard (1,250 pairs; the wide pre-tier needs
+    9 whole CUs per turning pair) runs: wide pairs whose parts are not all
+    resident give up after the first exchange's 4 ms wait, mark the pair's
+    slots so the partners stop at once, and run in the repair launch — the
+    batch ends in tens of ms, not at the end of the occupation, bit-identical
+    to an unoccupied run, the timeouts reported (tools/occupy_probe.py:
+    ~18 ms; with all but 8 CUs held even a one-kernel torch op waits out the
+    occupation, so that is not a test of the library)."""
+    import os
+    import select
+    import subprocess
+    import sys
+    import time
+    import torch
+    from conftest import PKG
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 1250
+    seq, inits = _sequence_pairs(n, seed=2025)
+    ss = k.ScanSet(seq.scans)
+    b = k.IcpBatch(ss, np.arange(1, n + 1), np.arange(0, n), inits, epsilon=0.05, max_iters=100)
+    b.launch()
+    ref = b.result()
+    assert lib.slam_icp_gang_timeouts() == 0
+    assert (np.abs(np.arctan2(inits[:, 1, 0], inits[:, 0, 0])) > 0.3).sum() >= 8   # wide pre-tier pairs
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    occ = subprocess.Popen([sys.executable, "-c", _OCCUPIER, PKG, str(n_cu - 32), "60000000"],   # 0.6 s
+                           stdout=subprocess.PIPE, text=True, env=dict(os.environ))
+    try:
+        ready, _, _ = select.select([occ.stdout], [], [], 90)
+        assert ready and occ.stdout.readline().strip() == "launched"
+        time.sleep(0.05)   # the occupying workgroups are resident
+        t0 = time.perf_counter()
+        b.launch()
+        done = torch.cuda.Event()
+        done.record()
+        done.synchronize()
+        dt = time.perf_counter() - t0
+        assert occ.wait(timeout=30) == 0
+    finally:
+        if occ.poll() is None:
+            occ.kill()
+    r = b.result()
+    assert np.array_equal(r.iters, ref.iters)
+    assert np.array_equal(r.tf, ref.tf) and np.array_equal(r.err, ref.err)
+    assert lib.slam_icp_gang_timeouts() > 0
+    assert dt < 0.15, dt
+
+
 @pytest.mark.parametrize("B", [9000, 5000, 4096, 1250, 37])
 def test_scheduler_order_is_a_stable_sort(B):
     """Phase 2's visiting order is the scheduler's stable bucket sort: the same

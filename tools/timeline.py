@@ -3,7 +3,9 @@ shard of the C3 stream (the 10k stream bench.py shards), when each pair's
 workgroup started and ended in each scheduler phase, where (XCC / CU), and
 what bounds the makespan.  GPU only.
 
-    python tools/timeline.py [N:rank ...]     (default 8:0 4:0; a bare P: the first P pairs)
+    python tools/timeline.py [N:rank ...]     (default 8:0 4:0; a bare P: the first P pairs;
+                                              bN:rank: rank's shard of slamhip.dist.balanced_shards)
+Environment: SHARD_SEED (2025).
 """
 import os
 import sys
@@ -22,7 +24,7 @@ def main():
     lib = _abi.lib()
     from slamhip import dist as sd
     specs = sys.argv[1:] or ["8:0", "4:0"]
-    seq = synthetic.make_sequence(10001, seed=2025)
+    seq = synthetic.make_sequence(10001, seed=int(os.environ.get("SHARD_SEED", "2025")))
     inits = np.stack([se2.pose_to_mat(seq.odometry[i] - seq.odometry[i - 1]) for i in range(1, 10001)])
     ss = k.ScanSet(seq.scans)
     full = k.IcpBatch(ss, np.arange(1, 10001), np.arange(0, 10000), inits, epsilon=0.05, max_iters=100)
@@ -32,15 +34,20 @@ def main():
     for nr in (2, 4, 8):
         mx = [int(it_all[sd.shard_range(10000, nr, r)[0]:sd.shard_range(10000, nr, r)[1]].max()) for r in range(nr)]
         print(f"N{nr}: longest pair per shard (iterations) {mx}", flush=True)
+    keys = sd.turn_keys(inits)
     for spec in specs:
-        if ":" in spec:
+        if spec.startswith("b"):
+            nr, r = (int(x) for x in spec[1:].split(":"))
+            idx = sd.balanced_shards(keys, nr)[r]
+        elif ":" in spec:
             nr, r = (int(x) for x in spec.split(":"))
             lo, hi, _ = sd.shard_range(10000, nr, r)
+            idx = np.arange(lo, hi)
         else:
-            lo, hi = 0, int(spec)
-        P = hi - lo
-        print(f"shard {spec}: pairs {lo}..{hi - 1}", flush=True)
-        b = k.IcpBatch(ss, np.arange(lo + 1, hi + 1), np.arange(lo, hi), inits[lo:hi], epsilon=0.05, max_iters=100)
+            idx = np.arange(0, int(spec))
+        P = len(idx)
+        print(f"shard {spec}: {P} pairs", flush=True)
+        b = k.IcpBatch(ss, idx + 1, idx, inits[idx], epsilon=0.05, max_iters=100)
         for _ in range(3):
             b.launch()
         torch.cuda.synchronize()
@@ -54,6 +61,7 @@ def main():
         lib.slam_icp_set_trace(None)
         ms = e0.elapsed_time(e1)
         it = b.result().iters
+        turn = keys[idx] > 0.3
         t = buf.cpu().numpy().reshape(P, 2, 4)
         st, en = t[:, :, 0].astype(np.float64), t[:, :, 1].astype(np.float64)
         ran = st > 0
@@ -75,12 +83,12 @@ def main():
         # finish-time quantiles and the last finishers
         q = np.nanpercentile(fin, [50, 90, 99, 100])
         print(f"   finish p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f} us", flush=True)
-        last = np.argsort(-np.nan_to_num(fin, nan=-1))[:12]
+        last = np.argsort(-np.nan_to_num(fin, nan=-1))[:16]
         for j in last:
             dur = (end2[j] - st2[j]) if not np.isnan(st2[j]) else np.nan
             rem = it[j] - 4
-            print(f"   pair {j:5d} iters {it[j]:3d} p1 {us(st[j, 0]):6.0f}-{end1[j]:6.0f} p2 {st2[j]:6.0f}-{end2[j]:6.0f}"
-                  f" ({dur / max(rem, 1):5.1f} us/it) xcc {int(t[j, 1, 2]) >> 32} hw {int(t[j, 1, 2]) & 0xffffffff:#x}",
+            print(f"   pair {j:5d}{'t' if turn[j] else ' '} iters {it[j]:3d} p1 {us(st[j, 0]):6.0f}-{end1[j]:6.0f} p2 {st2[j]:6.0f}-{end2[j]:6.0f}"
+                  f" ({dur / max(rem, 1):5.1f} us/it) xcc {int(t[j, 0, 2]) >> 32}/{int(t[j, 1, 2]) >> 32}",
                   flush=True)
         # how many pairs are running over time (phase 2)
         grid = np.arange(0, np.nanmax(fin) + 50, 50)

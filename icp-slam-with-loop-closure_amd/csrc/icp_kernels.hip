@@ -43,10 +43,11 @@ __device__ int g_icp_status;                // nonzero: some pair was outside it
 // (block_sum_exact16, alternating between iterations), then 16 doubles of
 // per-pair constants (kept in LDS, not in registers across the NN search)
 constexpr int kPairConsts = 42;   // 12 pair constants, then kBcast: the gang exchange's broadcast slab (16 sums + the
-                                  // arrival flag), then kKab: the update wave 0 hands to the others (an even count keeps
-                                  // the candidates 16-byte aligned)
+                                  // arrival flag), then kKab: the update wave 0 hands to the others and the drain
+                                  // flag (an even count keeps the candidates 16-byte aligned)
 __host__ __device__ constexpr int red_doubles(int block) { return 2 * (block / 64) * 16 + kPairConsts; }
-enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kPh0, kPhS, kBcast = 16, kKab = 34 };
+enum PairConst { kPcX, kPcY, kDpX, kDpY, kMupX, kMupY, kGm1, kGm2, kGs1, kGs2, kPmax, kCmax, kPh0, kPhS, kDrainAt,
+                 kBcast = 16, kKab = 34 };
 
 struct IcpArgs {
     const double2* pts;
@@ -110,6 +111,15 @@ struct IcpArgs {
     // padding (both: the workgroup leaves at once)
     const int32_t* skip_lt;
     const int32_t* take_lt;   // the pre-tier's launch: slots at or past *take_lt leave at once (NULL: none)
+    // drain (phase 2's bulk launch, launch_batch): *drain counts the launch's
+    // pairs that stopped (finished or paused); once at most drain_x of its
+    // *drain_n - drain_skip pairs have not, each pair pauses at the end of its
+    // iteration (those running and any still to start: at most drain_x) and
+    // the drain tier (wide workgroups) finishes them (NULL: off)
+    uint32_t* drain;
+    const int32_t* drain_n;
+    int32_t drain_skip;
+    int32_t drain_x;
 };
 constexpr int kGangMax = 17;          // parts per gang (1081-point scans: 17 groups of 64)
 #ifndef SLAM_TAIL_SHARE
@@ -994,6 +1004,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
     }
 
     if (tid == 0 && part == 0) trace_mark(a, b, 0);
+    // drain: the stopped-pair count at which the rest pause (in LDS: read once
+    // per iteration by wave 0, no register held through the loop)
+    if constexpr (!GANG && !STEP) {
+        if (a.drain && tid == 0) pconst[kDrainAt] = static_cast<double>(*a.drain_n - a.drain_skip - a.drain_x);
+    }
 #ifdef SLAM_ABL_STAGE2X
     // timing-only ablation: the staging twice (its cost = the difference)
     (void)stage_pair<BLOCK, SCREEN, PRUNE>(a, n1, n2, p1, p2, resident, cand, candf, box8, red0, red1, pconst);
@@ -1300,6 +1315,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         //   (p - c) m^T with p the untransformed pc1 point and c = pc1[0].
         // Then pc1_avg = T mu_p, and X Y^T = R_T [sum (p - c) m^T - dp pc2_avg^T]
         // (q - mu_q = R_T (p - mu_p) and sum (m - pc2_avg) = 0).
+        // drain count, read by wave 0 ahead of the sums' loads (used in the update)
+        uint32_t dword = 0;
+        if constexpr (!GANG && !STEP) {
+            if (a.drain && wave == 0)
+                dword = __hip_atomic_load(a.drain, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         double tot;
         {
             // the pc1 row is re-read (the untransformed point of the (p - c) m^T
@@ -1400,6 +1421,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                 pconst[kKab + 4] = Tn.m11;
                 pconst[kKab + 5] = Tn.m12;
                 pconst[kKab + 6] = err;
+                // drain: at most drain_x of the launch's pairs have not stopped
+                pconst[kKab + 7] =
+                    (!GANG && !STEP && a.drain && static_cast<double>(dword) >= pconst[kDrainAt]) ? 1.0 : 0.0;
             }
 #endif
         }
@@ -1412,6 +1436,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
         Tn.m11 = pconst[kKab + 4];
         Tn.m12 = pconst[kKab + 5];
         err = pconst[kKab + 6];
+        const bool drain_now = pconst[kKab + 7] != 0.0;
+#else
+        const bool drain_now = false;
 #endif
 
         stamp(3);
@@ -1461,10 +1488,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     a.out_err[b] = err;
                     a.out_iters[b] = it + 1;
                     trace_mark(a, b, 1);
+                    if (!GANG && a.drain) atomicAdd(a.drain, 1u);
                 }
                 return;
             }
-            if (a.phase_cap > 0 && it + 1 - it0 >= a.phase_cap) {
+            if ((a.phase_cap > 0 && it + 1 - it0 >= a.phase_cap) || drain_now) {
                 // pause (scheduler phase boundary): save the loop state; the
                 // last error change orders the survivors for the next phase
                 flush_stamps();
@@ -1492,6 +1520,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
                     a.out_iters[b] = -(it + 1);
                     a.sched_key[b] = static_cast<float>(derr);
                     trace_mark(a, b, 1);
+                    if (!GANG && a.drain) atomicAdd(a.drain, 1u);
                 }
                 return;
             }
@@ -2703,6 +2732,14 @@ static thread_local int g_angle_mix_share = 2;
 //        3.1-3.9 ms: 9 CUs per turning pair starve the bulk);
 //   larger batches: no tiers.
 static thread_local int g_sched_auto = 1;
+// drain tier (launch_batch): when at most this many of phase 2's bulk pairs
+// have not stopped, the running ones pause and finish on wide workgroups (-1:
+// kDrainPairs up to kSortOneMax pairs, none above; 0: off).  Measured on the
+// C3 shards (profiles/r06_drain_sweep2.txt, balanced, two rounds): 2 / 4 / 8
+// ranks 2.65-2.66 / 1.77-1.78 / 1.11-1.12 ms against 2.69 / 1.85-1.86 /
+// 1.13-1.17 without; 12, 16 and 28 pairs within noise of 24
+constexpr int kDrainPairs = 24;   // x 9 CU-exclusive workgroups (1081-point scans, two groups each): 216 CUs
+static thread_local int g_drain = -1;
 constexpr int kAutoSmall = 2048;
 constexpr int kAutoMidAngle = 96;
 constexpr int kAutoMidWide = 64;
@@ -2887,7 +2924,8 @@ __global__ __launch_bounds__(kSortBlock) void sched_count_kernel(const int32_t* 
 
 // One workgroup: hist_blk[blk][q] <- sum of the counts of all (q' < q, any
 // block) and (q, blk' < blk): the first slot of (bucket q, block blk).
-__global__ __launch_bounds__(512) void sched_scan_kernel(int32_t* __restrict__ hist_blk, int32_t nblk) {
+__global__ __launch_bounds__(512) void sched_scan_kernel(int32_t* __restrict__ hist_blk, int32_t nblk,
+                                                        int32_t* __restrict__ n_out) {
     __shared__ int chunk[kScanChunk * kNB];
     __shared__ int tot[512];
     const int q = threadIdx.x;
@@ -2917,6 +2955,7 @@ __global__ __launch_bounds__(512) void sched_scan_kernel(int32_t* __restrict__ h
         __syncthreads();
     }
     const int base = q < kNB ? tot[q] - run : 0;
+    if (n_out && q == kSchedBuckets) *n_out = base;   // the unfinished pairs (every bucket before the last)
     __syncthreads();
     tot[q] = base;
     __syncthreads();
@@ -2977,7 +3016,8 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
                                                                     const int32_t* __restrict__ ids,
                                                                     int32_t* __restrict__ k_dev,
                                                                     const double* __restrict__ init, int32_t kmax,
-                                                                    int32_t* __restrict__ out_iters, int32_t kmix = -1) {
+                                                                    int32_t* __restrict__ out_iters, int32_t kmix = -1,
+                                                                    int32_t* __restrict__ n_out = nullptr, int32_t koff0 = 0) {
     constexpr int WAVES = kSortBlock / 64;
     constexpr int PER = kSortOneMax / kSortBlock;
     __shared__ int base[kNB];
@@ -2985,7 +3025,10 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int64_t e = tid; e < nz; e += kSortBlock) zero[e] = 0;
     for (int i = tid; i < kNB; i += kSortBlock) base[i] = 0;
-    const int koff = (MODE == 0 && k_dev) ? *k_dev : 0;
+    const int koff = MODE == 0 ? (k_dev ? *k_dev : koff0) : 0;
+    if constexpr (MODE == 0) {   // ids may hold -1 padding (not placed): every slot starts as padding
+        for (int j = tid; j < B; j += kSortBlock) order[j] = -1;
+    }
     const int n = B - koff;   // entries sorted
     __syncthreads();
     int q[PER], pb[PER];
@@ -3021,6 +3064,7 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
             if (i < kNB) base[i] = carry + x - v;
             carry += __shfl(x, 63, 64);
         }
+        if (MODE == 0 && lane == 0 && n_out) *n_out = base[kSchedBuckets];   // the unfinished pairs sorted
         if constexpr (MODE == 1) {
             if (lane == 0) *k_dev = min(base[kSchedBuckets], kmax);   // turning pairs precede bucket 256
             if (lane == 0 && kmix >= 0) k_dev[1] = min(base[kSchedBuckets], kmix);   // the mixed pre-tier's wide part
@@ -3058,9 +3102,6 @@ __global__ __launch_bounds__(kSortBlock) void sched_sort_one_kernel(const int32_
             base[i] += t;
         }
         __syncthreads();
-    }
-    if constexpr (MODE == 0) {
-        for (int j = n + tid; j < B; j += kSortBlock) order[j] = -1;   // padding: those workgroups leave at once
     }
 }
 
@@ -3159,7 +3200,24 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     const size_t ap_bytes = ap ? ((nb + 2) * sizeof(int32_t) + 255) / 256 * 256 + ap_slot_words * sizeof(uint64_t) +
                                      static_cast<size_t>(ap) * wide_slab_f4(static_cast<int>(cand_cap_w)) * sizeof(float4)
                                : 0;
-    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes + ap_bytes;
+    // drain tier: the counters, then its pairs' exchange slots and fp32 candidates
+    // (default: batches up to the one-workgroup sort, the strong-scaling shards;
+    // the 10k batch ran 1 % slower with it, profiles/r06_drain_sweep2.txt)
+    const int drain_cfg = g_drain < 0 ? (B <= kSortOneMax ? kDrainPairs : 0) : g_drain;
+    // (a batch above the one-workgroup sort drains only without other phase-2
+    // tiers: its three-kernel sort takes every pair)
+    const bool one_sort = B <= kSortOneMax && g_sched_sort_one;
+    const int drain_x = drain_cfg > 0 && !bg && wide_ok && wide_lds_bytes(static_cast<int>(cand_cap_w), 2) <= kMaxLds &&
+                                (one_sort || (heads == 0 && ap == 0))
+                            ? drain_cfg
+                            : 0;
+    const size_t drain_slot_words = static_cast<size_t>(drain_x) * 2 * wide_parts * 32;
+    const size_t drain_bytes = drain_x ? 256 + (nb * sizeof(int32_t) + 255) / 256 * 256 + drain_slot_words * sizeof(uint64_t) +
+                                             static_cast<size_t>(drain_x) * wide_slab_f4(static_cast<int>(cand_cap_w)) *
+                                                 sizeof(float4)
+                                       : 0;
+    const size_t bytes =
+        sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes + ap_bytes + drain_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);   // hist_blk[nblk][kNB]
@@ -3175,6 +3233,13 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     int32_t* ap_k = ap ? order0 + nb : nullptr;
     uint64_t* ap_slots = ap ? reinterpret_cast<uint64_t*>(ap0 + ((nb + 2) * sizeof(int32_t) + 255) / 256 * 256) : nullptr;
     float2* ap_cand = ap ? reinterpret_cast<float2*>(ap_slots + ap_slot_words) : nullptr;
+    char* dr0 = static_cast<char*>(ws) + (bytes - drain_bytes);
+    uint32_t* drain_w = drain_x ? reinterpret_cast<uint32_t*>(dr0) : nullptr;
+    int32_t* drain_n = drain_x ? reinterpret_cast<int32_t*>(dr0 + 8) : nullptr;
+    int32_t* drain_order = drain_x ? reinterpret_cast<int32_t*>(dr0 + 256) : nullptr;
+    uint64_t* drain_slots =
+        drain_x ? reinterpret_cast<uint64_t*>(dr0 + 256 + (nb * sizeof(int32_t) + 255) / 256 * 256) : nullptr;
+    float2* drain_cand = drain_x ? reinterpret_cast<float2*>(drain_slots + drain_slot_words) : nullptr;
     IcpArgs a = args;
     a.phase_cap = probe;
     a.sched_key = key;
@@ -3238,20 +3303,53 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         // phase 2 gives pairs new slots: clear phase 1's granules (a pair restarted
         // from iteration 0 would otherwise meet another pair's old tags)
         if (bg) (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
+        if (drain_w) (void)hipMemsetAsync(drain_w, 0, sizeof(uint32_t), ms);
         if (B <= kSortOneMax && g_sched_sort_one) {
             // one launch on the phase boundary: the sort, and the exchange slots zeroed beside it
             hipLaunchKernelGGL(sched_sort_one_kernel<0>, dim3(1), dim3(kSortBlock), 0, ms, args.out_iters, key, B, thr,
                                order, gang_slots, static_cast<int64_t>(G + Wd > 0 ? gang_slot_bytes / sizeof(uint64_t) : 0),
-                               order0, ap_k, static_cast<const double*>(nullptr), 0, static_cast<int32_t*>(nullptr));
+                               order0, ap_k, static_cast<const double*>(nullptr), 0, static_cast<int32_t*>(nullptr), -1,
+                               drain_n);
         } else {
             if (G + Wd > 0) (void)hipMemsetAsync(gang_slots, 0, gang_slot_bytes, ms);
             hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, ms, args.out_iters, key, B, thr,
                                hist, bucket);
-            hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, ms, hist, nblk);
+            hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, ms, hist, nblk, drain_n);
             hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, ms, bucket, B, hist, order);
         }
         rc = check_launch("icp scheduler kernels");
     }
+    // drain tier, queued right behind phase 2's bulk launch on its stream: the
+    // bulk's pairs (order[skip..B), entries past the unfinished ones finished
+    // or padding) sorted again, the ones it paused (at most drain_x) first,
+    // then on wide workgroups from their paused state; a wide pair whose parts
+    // were not all resident is re-run on one workgroup (repair)
+    auto drain_tier = [&](hipStream_t st, int skip) -> int {
+        const float thr = args.stopping_thresh > 0.0 ? static_cast<float>(args.stopping_thresh) : 1e-4f;
+        if (one_sort) {
+            hipLaunchKernelGGL(sched_sort_one_kernel<0>, dim3(1), dim3(kSortBlock), 0, st, args.out_iters, key, B, thr,
+                               drain_order, drain_slots, static_cast<int64_t>(drain_slot_words),
+                               static_cast<const int32_t*>(order), static_cast<int32_t*>(nullptr),
+                               static_cast<const double*>(nullptr), 0, static_cast<int32_t*>(nullptr), -1,
+                               static_cast<int32_t*>(nullptr), skip);
+        } else {   // (no other tier: every pair is the bulk's)
+            (void)hipMemsetAsync(drain_slots, 0, drain_slot_words * sizeof(uint64_t), st);
+            hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, st, args.out_iters, key, B, thr,
+                               hist, bucket);
+            hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, st, hist, nblk, static_cast<int32_t*>(nullptr));
+            hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, st, bucket, B, hist, drain_order);
+        }
+        int r = check_launch("icp drain sort");
+        IcpArgs d = a;
+        d.order = drain_order;
+        d.skip_lt = nullptr;
+        d.take_lt = nullptr;
+        d.phase_cap = 0;
+        d.resume = 1;
+        if (r == 0) r = launch_wide(d, drain_x, max_n1, max_n2, st, drain_slots, drain_cand, 1, 2);
+        if (r == 0) r = launch(false, d, min(B, 2 * drain_x), max_n1, max_n2, st);
+        return r;
+    };
     if (rc == 0) {   // phase 2: the unfinished pairs, slowest-converging first
         a.phase_cap = 0;
         a.resume = 1;
@@ -3288,9 +3386,16 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             }
             IcpArgs t = a;
             t.order = order + H;
+            if (drain_x && !bg) {
+                t.drain = drain_w;
+                t.drain_n = drain_n;
+                t.drain_skip = H;
+                t.drain_x = drain_x;
+            }
             if (rc == 0)
                 rc = bg ? launch_bulk_gangs(t, B - H, bg, max_n2, side->stream, bulk_slots + static_cast<size_t>(H) * 2 * bg->parts * 32)
                         : launch(false, t, B - H, max_n1, max_n2, side->stream);
+            if (rc == 0 && t.drain) rc = drain_tier(side->stream, H);
             if (rc == 0 && (hipEventRecord(side->join, side->stream) != hipSuccess ||
                             hipEventRecord(side->join2, side->stream2) != hipSuccess ||
                             hipEventRecord(side->join3, side->stream3) != hipSuccess))
@@ -3319,7 +3424,17 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
             if (ms != s && (hipEventRecord(side0->join3, ms) != hipSuccess || hipStreamWaitEvent(s, side0->join3, 0) != hipSuccess ||
                             (mix > 0 && hipStreamWaitEvent(s, side0->join4, 0) != hipSuccess)))
                 rc = fail(SLAM_EHIP, "icp scheduler: wait");
-            if (rc == 0) rc = launch(false, a, B, max_n1, max_n2, stream);
+            if (rc == 0) {
+                IcpArgs t = a;
+                if (drain_x) {
+                    t.drain = drain_w;
+                    t.drain_n = drain_n;
+                    t.drain_skip = 0;
+                    t.drain_x = drain_x;
+                }
+                rc = launch(false, t, B, max_n1, max_n2, stream);
+                if (rc == 0 && t.drain) rc = drain_tier(as_stream(stream), 0);
+            }
             if (rc == 0 && ap) {   // the pre-tier's repair (its pairs are not in phase 2's order)
                 IcpArgs r = a;
                 r.order = order0;
@@ -3565,12 +3680,18 @@ int slam_icp_sched_sort(const int32_t* iters, const float* key, int32_t B, float
     int32_t* hist = static_cast<int32_t*>(ws);
     int32_t* bucket = hist + static_cast<size_t>(nblk) * kNB;
     hipLaunchKernelGGL(sched_count_kernel, dim3(nblk), dim3(kSortBlock), 0, s, iters, key, B, thresh, hist, bucket);
-    hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk);
+    hipLaunchKernelGGL(sched_scan_kernel, dim3(1), dim3(512), 0, s, hist, nblk, static_cast<int32_t*>(nullptr));
     hipLaunchKernelGGL(sched_scatter_kernel, dim3(nblk), dim3(kSortBlock), 0, s, bucket, B, hist, order);
     const int rc = check_launch("sched sort kernels");
     (void)hipFreeAsync(ws, s);
     return rc;
 }
+int slam_icp_set_drain(int pairs) {
+    if (pairs < -1 || pairs > 64) return fail(SLAM_EINVAL, "drain: pairs outside [-1, 64]");
+    g_drain = pairs;
+    return ok();
+}
+
 int slam_icp_set_schedule(int probe_iters, int min_pairs) {
     if (probe_iters < -1 || min_pairs < 0) return fail(SLAM_EINVAL, "schedule: probe_iters < -1 or min_pairs < 0");
     g_sched_probe = probe_iters;

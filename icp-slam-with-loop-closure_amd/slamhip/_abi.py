@@ -44,6 +44,7 @@ SIGNATURES = {
     "slam_icp_set_xcd_map": (c_int, [c_int]),
     "slam_icp_set_angle_tier": (c_int, [c_int, ctypes.c_float]),
     "slam_icp_set_schedule_auto": (c_int, [c_int]),
+    "slam_icp_set_drain": (c_int, [c_int]),
     "slam_icp_set_angle_tier_kind": (c_int, [c_int]),
     "slam_icp_set_angle_tier_mix": (c_int, [c_int, c_int]),
     "slam_icp_set_wide_groups": (c_int, [c_int]),

@@ -360,6 +360,14 @@ int slam_icp_set_wide_groups(int groups);
  * first 24 as gangs of 4; larger batches no tiers.  0: the explicit settings;
  * any of the tier setters above selects them, 1 restores their defaults too. */
 int slam_icp_set_schedule_auto(int on);
+/* The drain tier of phased batches: once every pair of phase 2's bulk launch
+ * has started and at most `pairs` still run, each of them pauses at the end of
+ * its iteration and they finish on wide workgroups (two query groups, one per
+ * CU), from their paused state, bit-identical.  -1: the default (24 for
+ * batches up to 8,192 pairs, off above), 0: off, at most 64 (more than
+ * 256 / parts pairs cannot all be resident: their exchanges time out and the
+ * repair launch finishes them). */
+int slam_icp_set_drain(int pairs);
 /* Diagnostics: the XCD-aware pair map of launches in stream order: runs of
  * `run` consecutive pairs per XCD (default 16, so consecutive pairs share
  * their common scan through one L2 while the runs rotate over the XCDs),

@@ -586,6 +586,46 @@ def test_gang_timeouts_are_repaired(k):
     assert lib.slam_icp_gang_timeouts() == 0
 
 
+def test_drain_tier_is_bit_identical(k):
+    """The drain tier (phase 2's last running pairs paused and finished on wide
+    workgroups): every setting, and forced exchange timeouts (the wide pairs
+    then finish in the repair launch), give the drain-off results bit for bit,
+    history included, on a 2,500-pair stream and a 10,000-pair-size batch path
+    (B > 8,192: the three-kernel sort)."""
+    from slamhip import _abi
+    lib = _abi.lib()
+    n = 2500
+    seq, inits = _sequence_pairs(n, seed=2025)
+    src, dst = np.arange(1, n + 1), np.arange(0, n)
+    try:
+        assert lib.slam_icp_set_drain(0) == 0
+        ref = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+        for d, wait in ((1, 0), (8, 0), (24, 0), (64, 0), (24, 1)):
+            assert lib.slam_icp_set_drain(d) == 0
+            assert lib.slam_icp_set_gang_wait(wait) == 0
+            lib.slam_icp_gang_timeouts()   # clear
+            r = k.icp_batch(seq.scans, src, dst, inits, epsilon=0.05, max_iters=100, history=True)
+            if wait:
+                assert lib.slam_icp_gang_timeouts() > 0, d
+            assert np.array_equal(r.iters, ref.iters), d
+            assert np.array_equal(r.tf, ref.tf) and np.array_equal(r.err, ref.err), d
+            for h0, h1 in zip(ref.hist, r.hist):
+                assert np.array_equal(h0, h1), d
+        # the large-batch path: 9,000 pairs (3 x the stream, B > 8,192)
+        assert lib.slam_icp_set_gang_wait(0) == 0
+        s3, d3, i3 = np.tile(src, 3)[:9000], np.tile(dst, 3)[:9000], np.tile(inits, (3, 1, 1))[:9000]
+        assert lib.slam_icp_set_drain(0) == 0
+        big0 = k.icp_batch(seq.scans, s3, d3, i3, epsilon=0.05, max_iters=100)
+        assert lib.slam_icp_set_drain(24) == 0
+        big1 = k.icp_batch(seq.scans, s3, d3, i3, epsilon=0.05, max_iters=100)
+        assert np.array_equal(big1.iters, big0.iters) and np.array_equal(big1.tf, big0.tf)
+        assert np.array_equal(big0.iters[:n], ref.iters) and np.array_equal(big0.tf[:n], ref.tf)
+    finally:
+        lib.slam_icp_set_gang_wait(0)
+        lib.slam_icp_set_drain(-1)
+    assert lib.slam_icp_gang_timeouts() == 0
+
+
 _OCCUPIER = """
 import sys, time
 sys.path.insert(0, sys.argv[1])

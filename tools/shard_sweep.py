@@ -2,7 +2,7 @@
 rank's shard of ONE C3 stream over N ranks (N = 2, 4, 8) timed on its own
 (HIP events, median of 5 launches), under each scheduler setting
 "heads,gangs,parts,wide,share[,probe[,sort_one[,tier_limit[,xcd_map[,angle_max[,angle_centirad[,angle_kind[,mix,mix_share]]]]]]]]"
-or "auto" (the library's automatic tier profile).  The projected N-GPU time
+or "auto" (the library's automatic tier profile; "auto:P" with a phase-1 probe of P iterations).  The projected N-GPU time
 is the slowest shard (bench.py takes the max over ranks).
 (bench.py --pairs P builds ANOTHER stream of P pairs: synthetic.make_sequence
 draws its noise after the whole trajectory, so a shorter stream is not a
@@ -13,7 +13,8 @@ prefix of the 10k one.)  GPU only.
 Environment: SHARD_TOTAL (10000 pairs), SHARD_N (2,4,8), SHARD_SEED (2025:
 the C3 stream), SHARD_DROPOUT (0: 1081-point scans; 0.35: ragged 700-1081),
 SHARD_MODE (contiguous | balanced | both: slamhip.dist.contiguous_shards /
-balanced_shards), SHARD_WIDE_GROUPS (query groups per wide-tier workgroup).
+balanced_shards), SHARD_WIDE_GROUPS (query groups per wide-tier workgroup),
+SHARD_DRAIN (drain tier pairs: -1 the default, 0 off).
 """
 import os
 import sys
@@ -32,6 +33,8 @@ def main():
     from slamhip import icp as k
     lib = _abi.lib()
     settings = sys.argv[1:] or ["auto"]
+    if os.environ.get("SHARD_DRAIN"):   # drain tier pairs (-1 default, 0 off)
+        assert lib.slam_icp_set_drain(int(os.environ["SHARD_DRAIN"])) == 0
     if os.environ.get("SHARD_WIDE_GROUPS"):   # query groups per wide-tier workgroup (1 or 2)
         assert lib.slam_icp_set_wide_groups(int(os.environ["SHARD_WIDE_GROUPS"])) == 0
     total = int(os.environ.get("SHARD_TOTAL", "10000"))
@@ -69,13 +72,13 @@ def main():
         return float(np.median(ts))
     try:
         for st in settings:
-            if st == "auto":   # the library's automatic tier profile by batch size
+            if st.startswith("auto"):   # the library's automatic tier profile by batch size ("auto:P": phase-1 probe P)
                 assert lib.slam_icp_set_schedule_auto(1) == 0
-                v = [0, 0, 4, 0, 1]
+                v = [0, 0, 4, 0, 1] + ([int(st[5:])] if st.startswith("auto:") else [])
             else:
                 v = [int(x) for x in st.split(",")]
             h, g, gp, w, ws = v[:5]
-            if st != "auto":
+            if not st.startswith("auto"):
                 assert lib.slam_icp_set_schedule_heads(h) == 0
                 assert lib.slam_icp_set_schedule_gangs(g, gp) == 0
                 assert lib.slam_icp_set_schedule_wide(w, ws) == 0
@@ -83,7 +86,7 @@ def main():
             assert lib.slam_icp_set_sched_sort_one(v[6] if len(v) > 6 else 1) == 0
             assert lib.slam_icp_set_tier_limit(v[7] if len(v) > 7 else 0) == 0
             assert lib.slam_icp_set_xcd_map(v[8] if len(v) > 8 else -1) == 0
-            if st != "auto":
+            if not st.startswith("auto"):
                 assert lib.slam_icp_set_angle_tier(v[9] if len(v) > 9 else 0, (v[10] if len(v) > 10 else 30) / 100.0) == 0
                 assert lib.slam_icp_set_angle_tier_kind(v[11] if len(v) > 11 else 0) == 0
                 assert lib.slam_icp_set_angle_tier_mix(v[12] if len(v) > 12 else 0, v[13] if len(v) > 13 else 2) == 0

@@ -1,6 +1,5 @@
 set -e
 export TMPDIR=/tmp
-SHARD_MODE=balanced SHARD_N=2,4 timeout -k 10 500 python -u tools/shard_sweep.py auto auto:2 auto:4 auto:5 auto:6 auto:8 2>&1 | grep -v amdgpu > gpurun_out/r06_probe_sweep.txt
 for r in 1 2; do
 SHARD_N=1 SHARD_MODE=balanced SHARD_WIDE_GROUPS=2 SHARD_DRAIN=0 timeout -k 10 300 python -u tools/shard_sweep.py auto 1,0,4,1,1,-1,1,10001 2,0,4,2,1,-1,1,10001 4,0,4,4,1,-1,1,10001 8,0,4,8,1,-1,1,10001 2>&1 | grep -v amdgpu >> gpurun_out/r06_wide10k_sweep.txt
 done

@@ -138,12 +138,16 @@ def tier_profile(B):
     (csrc/icp_kernels.hip launch_batch)."""
     if B < 1024:
         return "one launch, one workgroup per pair"
+    drain = "; drain tier: phase 2's last 24 running pairs on wide workgroups"
     if B < 2048:
-        return "two-phase; turning pairs (<= 40) on the wide pre-tier, 2 query groups per CU-exclusive workgroup"
+        return ("two-phase (probe 3); turning pairs (<= 40) on the wide pre-tier, 2 query groups per CU-exclusive"
+                " workgroup" + drain)
     if B < 4096:
-        return "two-phase; turning pairs (<= 64) on the wide pre-tier, 2 query groups per CU-exclusive workgroup"
+        return ("two-phase (probe 4); turning pairs (<= 64) on the wide pre-tier, 2 query groups per CU-exclusive"
+                " workgroup" + drain)
     if B <= 8192:
-        return "two-phase; turning pairs (<= 96) as gangs of 4; phase 2: 64 CU-exclusive heads, 24 as gangs of 4"
+        return ("two-phase (probe 2); turning pairs (<= 96) as gangs of 4; phase 2: 64 CU-exclusive heads, 24 as"
+                " gangs of 4" + drain)
     return "two-phase scheduler (phase 1: 3 iterations per pair; phase 2 slowest-first), no tiers"
 
 

@@ -2628,12 +2628,18 @@ static int launch(bool step, const IcpArgs& args, int32_t B, int32_t max_n1, int
 // ---------------------------------------------------------------------------
 constexpr int kSchedBuckets = 256;
 static thread_local int g_sched_probe = -1;   // phase-1 iterations (0: single launch; -1: automatic, sched_probe_for)
-// Automatic probe length (round 4, profiles/r04_probe_shards*.txt, C3 stream):
-// 3 iterations for the full batch (10k pairs: 4.09 ms; 2: 4.11, 4: 4.27) and
-// for 1,250 / 5,000-pair shards; 4 for 2,048-4,095 pairs, where the tail tiers
-// run and a longer probe keys them better (2,500 pairs: 2.03-2.04 ms against
-// 2.14-2.15 with 3; 1,250 pairs: 1.49 against 1.44)
-static int sched_probe_for(int B) { return B >= 2048 && B < 4096 ? 4 : 3; }
+// Automatic probe length.  Round 4 (profiles/r04_probe_shards*.txt, C3
+// stream): 3 iterations for the full batch (10k pairs: 4.09 ms; 2: 4.11, 4:
+// 4.27) and for 1,250 / 5,000-pair shards; 4 for 2,048-4,095 pairs, where the
+// tail tiers run and a longer probe keys them better (2,500 pairs: 2.03-2.04
+// ms against 2.14-2.15 with 3; 1,250 pairs: 1.49 against 1.44).  Round 6, at
+// the round-6 kernels and tiers, timed as bench.py times (20 back-to-back
+// launches, settings alternated on one box, profiles/r06_ab_probe*.txt): 2 for
+// 4,096-8,192 pairs (the 2-rank shards' maximum 2.55 / 2.71 ms on seeds 2025 /
+// 7, against 2.55 / 2.84 with 3 and 2.50 / 2.95 with 4); the 10k batch keeps 3
+// (3.97 / 4.33 ms against 4.03 / 4.19 with 2: a wash over the two seeds), the
+// 1,250-pair shards 3 (2: 1.08-1.09 against 1.03-1.06), 2,048-4,095 pairs 4
+static int sched_probe_for(int B) { return B >= 4096 && B <= 8192 ? 2 : B >= 2048 && B < 4096 ? 4 : 3; }
 static thread_local int g_sched_min_pairs = 1024;   // batches below this fit the GPU at once
 // Phase 2 starts the pairs the probe keyed slowest (the top g_sched_heads, at
 // most one per 16 pairs) on workgroups that request the whole LDS of a CU, so

@@ -265,7 +265,8 @@ int slam_icp_set_screen(int mode);
  * every pair runs probe_iters iterations, then the unfinished ones resume in
  * order of their last error change (slowest-converging first), so the long
  * tail of iteration counts does not start late.  probe_iters = 0: one launch;
- * -1 (default): automatic — 3, or 4 for batches of 2,048-4,095 pairs.
+ * -1 (default): automatic — 3, or 4 for batches of 2,048-4,095 pairs and 2
+ * for 4,096-8,192.
  * Defaults (-1, 1024).  Results are identical either way. */
 int slam_icp_set_schedule(int probe_iters, int min_pairs);
 /* Phase 2 of the scheduler starts the (at most) `heads` pairs the probe keyed

@@ -2,7 +2,9 @@
 back-to-back launches between two events, no sync between them), alternating settings on one
 box.   python tools/ab_probe.py [probe ...]  (default 3 2)
 Environment: AB_SHARD "N:r" times rank r's balanced shard of N ranks instead of the whole batch;
-AB_KNOB=drain: the values are drain-tier settings (slam_icp_set_drain) instead of probe lengths."""
+AB_KNOB=drain: the values are drain-tier settings (slam_icp_set_drain) instead of probe lengths;
+AB_KNOB=wide: the values are phase-2 wide heads (0: the automatic profile; n: n slowest-keyed pairs
+on wide workgroups of two query groups, every tier limit lifted)."""
 import os
 import sys
 
@@ -35,6 +37,17 @@ def main():
             for p in probes:
                 if os.environ.get("AB_KNOB") == "drain":
                     assert lib.slam_icp_set_drain(p) == 0
+                elif os.environ.get("AB_KNOB") == "wide":
+                    if p == 0:
+                        assert lib.slam_icp_set_schedule_auto(1) == 0
+                        assert lib.slam_icp_set_tier_limit(0) == 0
+                    else:
+                        assert lib.slam_icp_set_wide_groups(2) == 0
+                        assert lib.slam_icp_set_schedule_heads(p) == 0
+                        assert lib.slam_icp_set_schedule_gangs(0, 4) == 0
+                        assert lib.slam_icp_set_schedule_wide(p, 1) == 0
+                        assert lib.slam_icp_set_angle_tier(0, 0.3) == 0
+                        assert lib.slam_icp_set_tier_limit(100000) == 0
                 else:
                     assert lib.slam_icp_set_schedule(p, 1024) == 0
                 for _ in range(2):
@@ -53,6 +66,9 @@ def main():
                 assert np.array_equal(r.iters, ref.iters) and np.array_equal(r.tf, ref.tf)
         lib.slam_icp_set_schedule(-1, 1024)
         lib.slam_icp_set_drain(-1)
+        lib.slam_icp_set_tier_limit(0)
+        lib.slam_icp_set_wide_groups(1)
+        lib.slam_icp_set_schedule_auto(1)
         print(f"seed {seed} pairs {len(idx)}: " + " | ".join(f"{os.environ.get('AB_KNOB', 'probe')} {p}: " + " ".join(f"{t:.3f}" for t in res[p]) +
                                             f" (median {np.median(res[p]):.3f} ms)" for p in probes), flush=True)
 

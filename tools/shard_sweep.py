@@ -14,7 +14,9 @@ Environment: SHARD_TOTAL (10000 pairs), SHARD_N (2,4,8), SHARD_SEED (2025:
 the C3 stream), SHARD_DROPOUT (0: 1081-point scans; 0.35: ragged 700-1081),
 SHARD_MODE (contiguous | balanced | both: slamhip.dist.contiguous_shards /
 balanced_shards), SHARD_WIDE_GROUPS (query groups per wide-tier workgroup),
-SHARD_DRAIN (drain tier pairs: -1 the default, 0 off).
+SHARD_DRAIN (drain tier pairs: -1 the default, 0 off), SHARD_TIMING (b2b: 20 back-to-back launches
+per shard as bench.py times them, instead of the median of single launches, which also counts
+the host's enqueue of the scheduler's launches).
 """
 import os
 import sys
@@ -58,9 +60,20 @@ def main():
     ref = {}
     full = {}
 
+    b2b = os.environ.get("SHARD_TIMING") == "b2b"
+
     def timed(b, reps=5):
         b.launch()
         torch.cuda.synchronize()
+        if b2b:   # as bench.py times: 20 back-to-back launches between two events, per launch
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            b.launch()
+            e0.record()
+            for _ in range(20):
+                b.launch()
+            e1.record()
+            e1.synchronize()
+            return e0.elapsed_time(e1) / 20
         ts = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

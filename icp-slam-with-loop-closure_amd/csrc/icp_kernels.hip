@@ -92,6 +92,10 @@ struct IcpArgs {
     uint64_t* gang_slots;    // [n_gangs][2][gang][32] tagged granules, zeroed before the launch
     uint32_t gang_wait;      // longest wait for the partners of one exchange (s_memrealtime ticks)
     uint32_t gang_wait_first;   // the same for a launch's FIRST exchange of a pair (partners not resident)
+    // a word the launch's parts share (zeroed before it; NULL: none): the first
+    // part that times out at its first exchange sets it, and every part still
+    // waiting at, or later reaching, its own first exchange stops at once
+    uint32_t* gang_abort;
     // PRUNE kernels, scheduler phases: a paused pair's search state (per query
     // i: last match and clearance word at qsave[b * qsave_stride + i]; the
     // motion T_next - T and its slack at dtsave[b * 8 + ..]) so that its resumed
@@ -671,7 +675,8 @@ constexpr uint32_t kGangAbortTag = 0xffffffffu;
 // not all arrive within `wait` s_memrealtime ticks; the sum is then garbage.
 template <int N>
 __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp, int part, int parts, uint64_t tag,
-                                             uint32_t own, int lane, uint32_t wait, bool& arrived) {
+                                             uint32_t own, int lane, uint32_t wait, bool& arrived,
+                                             uint32_t* abortw) {
     uint32_t v[N];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     arrived = true;
@@ -694,9 +699,17 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
             arrived = false;
             break;
         }
+        // first exchange: another pair of the launch already found its partners absent
+        if (abortw && __hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            arrived = false;
+            break;
+        }
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > wait) {   // a partner never arrived
-            if (lane == 0) atomicAdd(&g_gang_timeout, 1);
+            if (lane == 0) {
+                atomicAdd(&g_gang_timeout, 1);
+                if (abortw) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             arrived = false;
             break;
         }
@@ -731,7 +744,7 @@ __device__ __forceinline__ double gang_sweep(const uint64_t* buf, int g, int pp,
 // part's until they all arrived (or `wait` ran out: arrived = false), and
 // return the total of value q in lane q < 16.  Called by ONE wave per part.
 __device__ __forceinline__ double gang_exchange_wave(double t, uint64_t* slots, int part, int parts, int e,
-                                                     uint32_t wait, bool& arrived) {
+                                                     uint32_t wait, bool& arrived, uint32_t* abortw = nullptr) {
     // an opaque lane index: the sweep's addresses are recomputed at every
     // exchange (a few VALU) instead of hoisted out of the ICP loop, where the
     // 16-wave wide instance (128 VGPRs) spilled them to scratch
@@ -749,13 +762,13 @@ __device__ __forceinline__ double gang_exchange_wave(double t, uint64_t* slots, 
     // branch-free sweeps of N loads per lane (a divergent guard around each
     // load made the compiler drain them one by one)
     if (parts <= 4)
-        s = gang_sweep<2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+        s = gang_sweep<2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived, abortw);
     else if (parts <= 8)
-        s = gang_sweep<4>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+        s = gang_sweep<4>(buf, g, pp, part, parts, tag, own, lane, wait, arrived, abortw);
     else if (parts <= 16)
-        s = gang_sweep<8>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+        s = gang_sweep<8>(buf, g, pp, part, parts, tag, own, lane, wait, arrived, abortw);
     else
-        s = gang_sweep<kGangSweep / 2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived);
+        s = gang_sweep<kGangSweep / 2>(buf, g, pp, part, parts, tag, own, lane, wait, arrived, abortw);
     if (!arrived) {   // (uniform) tell the partners: at this exchange and at the next (lanes 0-31 / 32-63)
         __hip_atomic_store(slots + ((e + (lane >> 5)) & 1) * parts * 32 + part * 32 + (lane & 31),
                            static_cast<uint64_t>(kGangAbortTag) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -767,12 +780,13 @@ __device__ __forceinline__ double gang_exchange_wave(double t, uint64_t* slots, 
 // arriver's loads) and broadcasts the sums and the arrival flag through LDS.
 // Returns false in every thread when a partner timed out.
 __device__ __forceinline__ bool gang_exchange(double& t, uint64_t* slots, int part, int parts, int e, uint32_t wait,
+                                             uint32_t* abortw,
                                              double* bcast) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     if (wave == 0) {
         bool arrived;
-        const double s = gang_exchange_wave(t, slots, part, parts, e, wait, arrived);
+        const double s = gang_exchange_wave(t, slots, part, parts, e, wait, arrived, abortw);
         if (lane < 16) bcast[lane] = s;
         if (lane == 0) bcast[16] = arrived ? 1.0 : 0.0;
     }
@@ -1361,7 +1375,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
             // a partner that never arrived: stop at once, write nothing (the
             // repair launch re-runs the pair from its phase-1 state)
             if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
-                                            parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, pconst + kBcast))
+                                            parts, it, it == it0 ? a.gang_wait_first : a.gang_wait,
+                                            it == it0 ? a.gang_abort : nullptr, pconst + kBcast))
                 return;
         }
         // The update is the same for every wave: wave 0 computes it and hands the
@@ -1872,7 +1887,8 @@ __global__ __launch_bounds__(kTeamBlock) void icp_team_kernel(IcpArgs a) {
             tot = block_sum_exact16<WAVES>(acc, ((it - it0) & 1) ? red0 : red1);
             tstamp(7);
             if (parts > 1 && !gang_exchange(tot, a.gang_slots + static_cast<int64_t>(slot) * 2 * parts * 32, part,
-                                            parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, pconst + kBcast)) {
+                                            parts, it, it == it0 ? a.gang_wait_first : a.gang_wait,
+                                            it == it0 ? a.gang_abort : nullptr, pconst + kBcast)) {
                 tflush();
                 return;   // a partner timed out: nothing written, the repair launch re-runs the pair
             }
@@ -2344,7 +2360,8 @@ __global__ __launch_bounds__(64 * kWideWaves * G) void icp_wide_kernel(IcpArgs a
             tstamp(4);
             bool arrived = true;
             if (parts > 1)
-                tot = gang_exchange_wave(tot, slots, part, parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, arrived);
+                tot = gang_exchange_wave(tot, slots, part, parts, it, it == it0 ? a.gang_wait_first : a.gang_wait, arrived,
+                                         it == it0 ? a.gang_abort : nullptr);
             tstamp(5);
             double flag = 0.0;
             if (!arrived) {
@@ -3222,8 +3239,10 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                                              static_cast<size_t>(drain_x) * wide_slab_f4(static_cast<int>(cand_cap_w)) *
                                                  sizeof(float4)
                                        : 0;
-    const size_t bytes =
-        sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes + ap_bytes + drain_bytes;
+    // one abort word per exchange-tier launch (IcpArgs::gang_abort), zeroed up front
+    constexpr size_t abort_bytes = 256;
+    const size_t bytes = sched_bytes + gang_slot_bytes + wide_cand_bytes + bulk_slot_bytes + qsave_bytes + ap_bytes +
+                         drain_bytes + abort_bytes;
     void* ws = nullptr;
     if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return fail(SLAM_EHIP, "icp scheduler: no workspace");
     int32_t* hist = static_cast<int32_t*>(ws);   // hist_blk[nblk][kNB]
@@ -3239,7 +3258,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
     int32_t* ap_k = ap ? order0 + nb : nullptr;
     uint64_t* ap_slots = ap ? reinterpret_cast<uint64_t*>(ap0 + ((nb + 2) * sizeof(int32_t) + 255) / 256 * 256) : nullptr;
     float2* ap_cand = ap ? reinterpret_cast<float2*>(ap_slots + ap_slot_words) : nullptr;
-    char* dr0 = static_cast<char*>(ws) + (bytes - drain_bytes);
+    char* dr0 = static_cast<char*>(ws) + (bytes - abort_bytes - drain_bytes);
+    uint32_t* abortw = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + (bytes - abort_bytes));
+    (void)hipMemsetAsync(abortw, 0, abort_bytes, s);
     uint32_t* drain_w = drain_x ? reinterpret_cast<uint32_t*>(dr0) : nullptr;
     int32_t* drain_n = drain_x ? reinterpret_cast<int32_t*>(dr0 + 8) : nullptr;
     int32_t* drain_order = drain_x ? reinterpret_cast<int32_t*>(dr0 + 256) : nullptr;
@@ -3281,9 +3302,11 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         IcpArgs w = args;
         w.order = order0;
         w.take_lt = ap_k;
+        w.gang_abort = abortw + 0;
         if (rc == 0 && mix > 0) {   // the largest turns on wide workgroups (slots below ap_k[1]), on
             IcpArgs wm = w;         // stream4 beside the gangs (joined back before the repair launches)
             wm.take_lt = ap_k + 1;
+            wm.gang_abort = abortw + 1;
             rc = launch_wide(wm, mix, max_n1, max_n2, side0->stream4, ap_slots, ap_cand, cfg_mix_share, cfg_groups);
             if (rc == 0 && hipEventRecord(side0->join4, side0->stream4) != hipSuccess) rc = fail(SLAM_EHIP, "icp scheduler: join");
             w.skip_lt = ap_k + 1;   // the gangs take the slots from there to ap_k[0]
@@ -3300,7 +3323,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         // as "not started" (out_iters 0) in phase 2, never as a stale result
         (void)hipMemsetAsync(args.out_iters, 0, nb * sizeof(int32_t), s);
         (void)hipMemsetAsync(bulk_slots, 0, bulk_slot_bytes, s);
-        rc = launch_bulk_gangs(a, B, bg, max_n2, s, bulk_slots);
+        IcpArgs a1 = a;
+        a1.gang_abort = abortw + 2;
+        rc = launch_bulk_gangs(a1, B, bg, max_n2, s, bulk_slots);
     } else {
         rc = launch(false, a, B, max_n1, max_n2, ms);
     }
@@ -3352,7 +3377,9 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
         d.take_lt = nullptr;
         d.phase_cap = 0;
         d.resume = 1;
+        d.gang_abort = abortw + 6;
         if (r == 0) r = launch_wide(d, drain_x, max_n1, max_n2, st, drain_slots, drain_cand, 1, 2);
+        d.gang_abort = nullptr;
         if (r == 0) r = launch(false, d, min(B, 2 * drain_x), max_n1, max_n2, st);
         return r;
     };
@@ -3378,11 +3405,15 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 hipStreamWaitEvent(side->stream3, side->fork, 0) != hipSuccess)
                 rc = fail(SLAM_EHIP, "icp scheduler: fork");
             // the wide tier on its own stream (the gangs must not queue behind it)
-            if (rc == 0 && Wd > 0)
-                rc = launch_wide(a, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand, cfg_share, cfg_groups);
+            if (rc == 0 && Wd > 0) {
+                IcpArgs aw = a;
+                aw.gang_abort = abortw + 3;
+                rc = launch_wide(aw, Wd, max_n1, max_n2, side->stream3, gang_slots, wide_cand, cfg_share, cfg_groups);
+            }
             if (rc == 0 && G > 0) {
                 IcpArgs g = a;
                 g.order = order + Wd;
+                g.gang_abort = abortw + 4;
                 rc = launch_gangs(g, G, parts, team, max_n1, max_n2, ms, gang_slots + wide_slot_words);
             }
             if (rc == 0 && H > GW) {
@@ -3398,6 +3429,7 @@ static int launch_batch(const IcpArgs& args, int32_t B, int32_t max_n1, int32_t 
                 t.drain_skip = H;
                 t.drain_x = drain_x;
             }
+            if (bg) t.gang_abort = abortw + 5;
             if (rc == 0)
                 rc = bg ? launch_bulk_gangs(t, B - H, bg, max_n2, side->stream, bulk_slots + static_cast<size_t>(H) * 2 * bg->parts * 32)
                         : launch(false, t, B - H, max_n1, max_n2, side->stream);

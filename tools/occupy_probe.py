@@ -68,6 +68,7 @@ def main():
         lib.slam_icp_set_schedule_heads(0)
         lib.slam_icp_set_schedule_wide(0, 1)
         lib.slam_icp_set_angle_tier(0, 0.3)
+        lib.slam_icp_set_gang_first_wait(0)   # (the drain tier still runs: its first-exchange wait)
 
     def auto():
         lib.slam_icp_set_schedule_auto(1)

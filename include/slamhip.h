@@ -310,7 +310,9 @@ int slam_icp_set_schedule_warm(int on);
  * exchange of a launch (a partner that is not resident by then, e.g. CUs held
  * by another process), 0.2 s later on.  Such a part stops at once without
  * writing and marks its next exchange so that partners already past this one
- * stop there too; after phase 2 the scheduler re-runs every exchange-tier pair
+ * stop there too; a first-exchange timeout also stops every other pair of the
+ * same launch at its first exchange (one wait per launch, not per pair);
+ * after phase 2 the scheduler re-runs every exchange-tier pair
  * that did not finish on one workgroup from its saved state, so the results
  * stay valid (and bit-identical): this count is a warning, not an error.
  * Scheduler order is a stable sort (deterministic). */
